@@ -1,0 +1,52 @@
+"""The oracle is pinned against the reference's own fixtures (bit for bit)
+and against the regenerated 1024 golden vectors (SHA-256)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+import golden_io as G
+
+
+@pytest.mark.parametrize("T", ["float", "double"])
+def test_stage1_matches_ref_fixture_64(T):
+    A = G.ref_bin(f"test_{T}_64_64.bin", 64, T)
+    band = oracle.brd_p1(A, 4)
+    assert np.array_equal(band, G.ref_bin(f"band_{T}_64_64.bin", 64, T))
+
+
+@pytest.mark.parametrize("T", ["float", "double"])
+def test_stage2_matches_ref_fixture_64(T):
+    band = G.ref_bin(f"band_{T}_64_64.bin", 64, T)
+    out, d, e = oracle.brd_p2(band, 4)
+    ref = G.ref_bin(f"bidiagonal_{T}_64_64.bin", 64, T)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(d, np.diagonal(ref)) and np.array_equal(e, np.diagonal(ref, 1))
+
+
+@pytest.mark.parametrize("T", ["float", "double"])
+def test_both_stages_match_ref_fixture_512(T):
+    man = G.manifest()["ref_data"]
+    A = G.ref_bin(f"test_{T}_512_512.bin", 512, T)
+    band = oracle.brd_p1(A, 4)
+    assert G.sha(band) == man[f"band_{T}_512_512.bin"]
+    out, _, _ = oracle.brd_p2(band, 4)
+    assert G.sha(out) == man[f"bidiagonal_{T}_512_512.bin"]
+    r = G.npz("ref512.npz")
+    assert np.array_equal(G.diags(band, -1, 5), r[f"band_{T}"])
+    assert np.array_equal(G.diags(out, -1, 2), r[f"bidiagonal_{T}"])
+
+
+@pytest.mark.parametrize("T", ["float", "double"])
+def test_gen1024_b32(T):
+    man = G.manifest()["gen1024"]
+    A = G.input1024(T)
+    assert G.sha(A) == man[f"test_{T}"]
+    band = oracle.brd_p1(A, 32)
+    assert G.sha(band) == man[f"band_{T}_b32"]
+    out, _, _ = oracle.brd_p2(band, 32)
+    assert G.sha(out) == man[f"bidiagonal_{T}_b32"]
+
+
+def test_oracle_rejects_bad_tile():
+    with pytest.raises(ValueError):
+        oracle.brd_p1(np.ones((10, 10)), 4)

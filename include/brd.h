@@ -1,0 +1,90 @@
+/*
+ * brd.h -- C ABI of the MI355X-native two-stage bidiagonal reduction
+ * (libbrd_hip.so, built from svdsolver_amd/csrc/).
+ *
+ * Plain pointers and sizes; no exceptions, no C++ or torch types cross this
+ * boundary.  Every entry point returns BRD_OK (0) or a negative brd_status;
+ * brd_last_error() gives a human-readable message for the calling thread.
+ *
+ * Storage: row-major (the layout of csc586::gpu::Matrix<T>::flatten(),
+ * matrix_gpu.h:223), element (i,j) at A[i*lda + j].
+ *
+ * Which reference interface each entry point replaces:
+ *   brd_ge2band_*   csc586::gpu::cuda_brd_p1(Matrix<float>& A, size_t b)
+ *                   (reference svd_cuda_2.cu:1117; svd_cuda_1.cu:750) and the
+ *                   CPU csc586::parallel::brd_p1<T>(Matrix<T>&, size_t)
+ *                   (svd_parallel.h:411).  Dense N x N -> upper band with b
+ *                   super-diagonals, in place.  Unlike the reference GPU path
+ *                   it is not fp32-only.
+ *   brd_band2bd_*   csc586::parallel::brd_p2<T>(Matrix<T>&, size_t b)
+ *                   (svd_parallel.h:640; twin gpu::brd_p2, svd_cpu.h:631) --
+ *                   band -> bidiagonal, in place, returning d and e like the
+ *                   reference's Bidiagonal{d, e} (svd_parallel.h:691).
+ *   brd_dist_*      new (the reference has no multi-GPU path):
+ *                   RCCL communicator for the block-column-sharded stage 1.
+ */
+#ifndef BRD_H_
+#define BRD_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum brd_status {
+    BRD_OK = 0,
+    BRD_EINVAL = -1,      /* bad argument (sizes, band width, null pointer)        */
+    BRD_EHIP = -2,        /* HIP runtime error (message in brd_last_error)         */
+    BRD_ENOMEM = -3,      /* device allocation failed                              */
+    BRD_ERCCL = -4,       /* RCCL error                                            */
+    BRD_EUNSUPPORTED = -5 /* valid request this build does not implement           */
+};
+
+/* flags */
+#define BRD_DEVICE_PTR 0x1u   /* A, d, e are device pointers (else host; staged)   */
+#define BRD_ASYNC      0x2u   /* device pointers only: return without syncing      */
+#define BRD_COMPAT     0x0u   /* stage 2: the reference's window geometry (default)*/
+#define BRD_EXACT_ORDER 0x4u  /* stage 2 compat, evaluated in the reference's exact
+                                 operation order (bit-identical to the reference's
+                                 CPU code; slow, for verification)                 */
+#define BRD_NO_EXTRACT 0x8u   /* stage 2: do not write d/e (may pass NULL)         */
+
+/* Stage 1: dense m x n (m >= n) -> upper band, bandwidth b (1 <= b <= 32).
+ * On return A holds the band matrix: entries (i,j) with 0 <= j-i <= b, and
+ * exact zeros elsewhere.  ngpus must be 1, or equal to the world size given
+ * to brd_dist_init (then A is this rank's column shard, see brd_dist_*). */
+int brd_ge2band_f64(double *A, int m, int n, int lda, int b, int ngpus, unsigned flags);
+int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned flags);
+
+/* Stage 2: n x n band (bandwidth b) -> bidiagonal, in place, with the
+ * reference's window geometry (BRD_COMPAT).  d (n) and e (n-1) receive the
+ * diagonal and super-diagonal (same memory kind as A). */
+int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags);
+int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags);
+
+/* Stream used by subsequent calls on this thread's device (hipStream_t; NULL =
+ * the library's own stream). */
+int brd_set_stream(void *hip_stream);
+
+/* Per-kernel device timing for roofline reporting.  While enabled, the library
+ * brackets every launch of the named kernel class with HIP events on the
+ * launch stream.  kernel: "s1_apply", "s1_factor", "s2_sweep".  Returns the
+ * number of launches, their total device time in ms and the algorithmic flops
+ * and bytes those launches were credited with. */
+int brd_profile_enable(int enable);
+int brd_profile_reset(void);
+int brd_profile_query(const char *kernel, long long *launches, double *total_ms,
+                      double *flops, double *bytes);
+
+/* Multi-GPU (one process per GPU, RCCL over xGMI). */
+int brd_dist_unique_id(void *id_out, int id_bytes);      /* id_bytes >= 128 */
+int brd_dist_init(int rank, int nranks, const void *id, int id_bytes);
+int brd_dist_finalize(void);
+
+const char *brd_last_error(void);
+int brd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BRD_H_ */

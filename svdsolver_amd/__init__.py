@@ -1,0 +1,11 @@
+"""svdsolver_amd: MI355X-native two-stage bidiagonal reduction (dense -> band
+-> bidiagonal), a drop-in for the GPU path of scrose/SVDSolver.
+
+The compute path is libbrd_hip.so (hand-written gfx950 HIP kernels behind the
+C ABI in include/brd.h); this package is its Python host side.
+"""
+from .brd import (BRD_DEVICE_PTR, BRD_EXACT_ORDER, BRD_NO_EXTRACT, BrdError, LIB_PATH,  # noqa: F401
+                  band2bd, brd_p1, brd_p2, cuda_brd_p1, ge2band, lib, profile_enable,
+                  profile_query, profile_reset)
+
+__all__ = ["ge2band", "band2bd", "brd_p1", "brd_p2", "cuda_brd_p1", "BrdError"]

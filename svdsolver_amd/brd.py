@@ -1,0 +1,202 @@
+"""Python host side of the MI355X two-stage bidiagonal reduction.
+
+Mirrors the reference's operator interface for the hot path:
+
+* :func:`brd_p1` / :func:`cuda_brd_p1` -- dense -> band, like
+  ``csc586::gpu::cuda_brd_p1(Matrix<float>& A, size_t b)`` (reference
+  svd_cuda_2.cu:1117) and ``csc586::parallel::brd_p1<T>`` (svd_parallel.h:411):
+  takes an N x N matrix and the band width b, returns the band matrix.
+* :func:`brd_p2` -- band -> bidiagonal with the reference's window geometry,
+  like ``csc586::parallel::brd_p2<T>`` (svd_parallel.h:640): returns the
+  matrix after the sweeps plus the ``Bidiagonal{d, e}`` vectors.
+
+Every call goes through the C ABI of ``lib/libbrd_hip.so`` (include/brd.h).
+numpy arrays take the host-pointer path (the library stages them through
+HBM); torch CUDA tensors are reduced in place on the device, on torch's
+current stream.  There is no CPU fallback: if the HIP library is missing the
+import of this module fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbrd_hip.so")
+
+BRD_DEVICE_PTR = 0x1
+BRD_ASYNC = 0x2
+BRD_COMPAT = 0x0
+BRD_EXACT_ORDER = 0x4
+BRD_NO_EXTRACT = 0x8
+
+EXPORTED = (
+    "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
+    "brd_set_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
+    "brd_dist_unique_id", "brd_dist_init", "brd_dist_finalize", "brd_last_error",
+    "brd_version",
+)
+
+
+class BrdError(RuntimeError):
+    """Raised when a libbrd_hip entry point returns a negative brd_status."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make -C svdsolver_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ci, cu = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint
+    for t in ("f64", "f32"):
+        f = getattr(L, f"brd_ge2band_{t}")
+        f.argtypes = [vp, ci, ci, ci, ci, ci, cu]
+        f.restype = ci
+        g = getattr(L, f"brd_band2bd_{t}")
+        g.argtypes = [vp, ci, ci, ci, vp, vp, cu]
+        g.restype = ci
+    L.brd_set_stream.argtypes = [vp]
+    L.brd_set_stream.restype = ci
+    L.brd_profile_enable.argtypes = [ci]
+    L.brd_profile_enable.restype = ci
+    L.brd_profile_reset.argtypes = []
+    L.brd_profile_reset.restype = ci
+    L.brd_profile_query.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong),
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_double)]
+    L.brd_profile_query.restype = ci
+    L.brd_dist_unique_id.argtypes = [vp, ci]
+    L.brd_dist_unique_id.restype = ci
+    L.brd_dist_init.argtypes = [ci, ci, vp, ci]
+    L.brd_dist_init.restype = ci
+    L.brd_dist_finalize.argtypes = []
+    L.brd_dist_finalize.restype = ci
+    L.brd_last_error.argtypes = []
+    L.brd_last_error.restype = ctypes.c_char_p
+    L.brd_version.argtypes = []
+    L.brd_version.restype = ci
+    return L
+
+
+lib = _load()
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != 0:
+        raise BrdError(fn, rc, lib.brd_last_error().decode(errors="replace"))
+
+
+def _sfx(dtype) -> str:
+    s = str(dtype)
+    if s in ("float64", "torch.float64"):
+        return "f64"
+    if s in ("float32", "torch.float32"):
+        return "f32"
+    raise TypeError(f"unsupported dtype {dtype} (float32 / float64 only)")
+
+
+def _is_torch_cuda(x) -> bool:
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+def _bind_stream(x) -> None:
+    import torch
+    lib.brd_set_stream(ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+
+
+# ---------------------------------------------------------------------------
+# stage 1
+# ---------------------------------------------------------------------------
+def ge2band(A, b: int, *, sync: bool = True):
+    """Dense -> band (bandwidth ``b``) IN PLACE.  ``A`` is a C-contiguous
+    float32/float64 numpy array (host path) or torch CUDA tensor (device
+    path, torch's current stream).  Returns ``A``."""
+    m, n = A.shape
+    sfx = _sfx(A.dtype)
+    fn = f"brd_ge2band_{sfx}"
+    if _is_torch_cuda(A):
+        assert A.is_contiguous(), "A must be contiguous"
+        _bind_stream(A)
+        flags = BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
+        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), m, n, n, int(b), 1, flags))
+    else:
+        if not (isinstance(A, np.ndarray) and A.flags.c_contiguous):
+            raise TypeError("host path needs a C-contiguous numpy array")
+        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.ctypes.data), m, n, n, int(b), 1, 0))
+    return A
+
+
+def brd_p1(A, b: int):
+    """Reference-compatible dense -> band: returns the band matrix (a copy for
+    numpy input, like ``csc586::parallel::brd_p1`` returning ``Matrix``)."""
+    if _is_torch_cuda(A):
+        return ge2band(A.contiguous().clone(), b)
+    return ge2band(np.array(A, copy=True, order="C"), b)
+
+
+cuda_brd_p1 = brd_p1   # name of the reference GPU entry point (svd_cuda_2.cu:1117)
+
+
+# ---------------------------------------------------------------------------
+# stage 2
+# ---------------------------------------------------------------------------
+def band2bd(A, b: int, *, exact_order: bool = False, sync: bool = True, extract: bool = True):
+    """Band -> bidiagonal IN PLACE with the reference's window geometry.
+    Returns (d, e) (None, None when ``extract`` is False)."""
+    m, n = A.shape
+    assert m == n, "stage 2 takes a square band matrix"
+    sfx = _sfx(A.dtype)
+    fn = f"brd_band2bd_{sfx}"
+    flags = (BRD_EXACT_ORDER if exact_order else 0) | (0 if extract else BRD_NO_EXTRACT)
+    if _is_torch_cuda(A):
+        import torch
+        _bind_stream(A)
+        d = torch.empty(n, dtype=A.dtype, device=A.device) if extract else None
+        e = torch.empty(max(n - 1, 1), dtype=A.dtype, device=A.device) if extract else None
+        flags |= BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
+        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), n, n, int(b),
+                                    ctypes.c_void_p(d.data_ptr() if extract else 0),
+                                    ctypes.c_void_p(e.data_ptr() if extract else 0), flags))
+        return (d, e[: n - 1]) if extract else (None, None)
+    if not (isinstance(A, np.ndarray) and A.flags.c_contiguous):
+        raise TypeError("host path needs a C-contiguous numpy array")
+    d = np.zeros(n, dtype=A.dtype)
+    e = np.zeros(max(n - 1, 1), dtype=A.dtype)
+    _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.ctypes.data), n, n, int(b),
+                                ctypes.c_void_p(d.ctypes.data), ctypes.c_void_p(e.ctypes.data), flags))
+    return (d, e[: n - 1]) if extract else (None, None)
+
+
+def brd_p2(A, b: int, *, exact_order: bool = False) -> Tuple[object, object, object]:
+    """Reference-compatible band -> bidiagonal: returns (A_after, d, e), where
+    A_after is what the reference writes to bidiagonal_*.bin."""
+    B = A.contiguous().clone() if _is_torch_cuda(A) else np.array(A, copy=True, order="C")
+    d, e = band2bd(B, b, exact_order=exact_order)
+    return B, d, e
+
+
+# ---------------------------------------------------------------------------
+# profiling (per-kernel HIP-event timing inside the library)
+# ---------------------------------------------------------------------------
+def profile_enable(on: bool = True) -> None:
+    _check("brd_profile_enable", lib.brd_profile_enable(1 if on else 0))
+
+
+def profile_reset() -> None:
+    _check("brd_profile_reset", lib.brd_profile_reset())
+
+
+def profile_query(kernel: str) -> dict:
+    n = ctypes.c_longlong()
+    ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    _check("brd_profile_query", lib.brd_profile_query(kernel.encode(), ctypes.byref(n), ctypes.byref(ms),
+                                                      ctypes.byref(fl), ctypes.byref(by)))
+    return {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}

@@ -1,0 +1,394 @@
+// C ABI of libbrd_hip.so (include/brd.h): argument checking, host<->device
+// staging, workspace management, the stage-1 panel loop and the stage-2
+// launch.  All GPU work is enqueued on one HIP stream.
+#include "brd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "brd_internal.h"
+
+namespace brd {
+
+// --------------------------------------------------------------------------
+// error reporting
+// --------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(BRD_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),  \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+// --------------------------------------------------------------------------
+// reduction tree
+// --------------------------------------------------------------------------
+Tree make_tree(int M, int bk) {
+    Tree t;
+    t.M = M;
+    t.bk = bk;
+    t.G0 = std::max(1, (M + kRmax - 1) / kRmax);
+    t.F = kRmax / std::max(bk, 1);
+    t.nlevels = 1;
+    t.lv[0] = {0, t.G0, 1, 0};
+    int prev = t.G0, stride = 1;
+    while (prev > 1) {
+        const int l = t.nlevels;
+        const int g = (prev + t.F - 1) / t.F;
+        t.lv[l] = {l, g, stride, prev};
+        stride *= t.F;
+        prev = g;
+        ++t.nlevels;
+    }
+    return t;
+}
+
+static size_t group_elems() { return (size_t)kRmax * 32 * 2 + 32 * 32; }
+
+size_t tree_ws_bytes(const Tree &t, size_t elem) {
+    size_t e = 0;
+    for (int l = 0; l < t.nlevels; ++l) e += (size_t)t.lv[l].groups * group_elems();
+    return e * elem;
+}
+
+void tree_ws_carve(const Tree &t, size_t elem, void *base, TreeWs &ws) {
+    char *p = (char *)base;
+    for (int l = 0; l < t.nlevels; ++l) {
+        const size_t g = t.lv[l].groups;
+        ws.V[l] = p;  p += g * kRmax * 32 * elem;
+        ws.VT[l] = p; p += g * 32 * kRmax * elem;
+        ws.T[l] = p;  p += g * 32 * 32 * elem;
+    }
+}
+
+// --------------------------------------------------------------------------
+// context: stream, workspace, profiling
+// --------------------------------------------------------------------------
+struct ProfAcc {
+    long long launches = 0;
+    double ms = 0, flops = 0, bytes = 0;
+};
+struct Pending {
+    std::string kind;
+    hipEvent_t a, b;
+    double flops, bytes;
+};
+
+struct Ctx {
+    std::mutex mu;
+    hipStream_t user_stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    bool prof = false;
+    std::map<std::string, ProfAcc> acc;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+static Ctx g_ctx;
+
+static hipStream_t stream() {
+    if (g_ctx.user_stream) return g_ctx.user_stream;
+    if (!g_ctx.own_stream) hipStreamCreateWithFlags(&g_ctx.own_stream, hipStreamNonBlocking);
+    return g_ctx.own_stream;
+}
+
+static int ensure_ws(size_t bytes) {
+    if (bytes <= g_ctx.ws_bytes) return BRD_OK;
+    if (g_ctx.ws) {
+        hipStreamSynchronize(stream());
+        hipFree(g_ctx.ws);
+        g_ctx.ws = nullptr;
+        g_ctx.ws_bytes = 0;
+    }
+    if (hipMalloc(&g_ctx.ws, bytes) != hipSuccess)
+        return fail(BRD_ENOMEM, "workspace allocation of %zu bytes failed", bytes);
+    g_ctx.ws_bytes = bytes;
+    return BRD_OK;
+}
+
+static hipEvent_t get_event() {
+    if (!g_ctx.event_pool.empty()) {
+        hipEvent_t e = g_ctx.event_pool.back();
+        g_ctx.event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct ProfScope {
+    bool on;
+    Pending p;
+    hipStream_t s;
+    ProfScope(const char *kind, double flops, double bytes, hipStream_t s_) : on(g_ctx.prof), s(s_) {
+        if (!on) return;
+        p.kind = kind;
+        p.flops = flops;
+        p.bytes = bytes;
+        p.a = get_event();
+        p.b = get_event();
+        hipEventRecord(p.a, s);
+    }
+    ~ProfScope() {
+        if (!on) return;
+        hipEventRecord(p.b, s);
+        g_ctx.pending.push_back(p);
+    }
+};
+
+static void prof_drain() {
+    for (auto &p : g_ctx.pending) {
+        hipEventSynchronize(p.b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        ProfAcc &a = g_ctx.acc[p.kind];
+        a.launches += 1;
+        a.ms += ms;
+        a.flops += p.flops;
+        a.bytes += p.bytes;
+        g_ctx.event_pool.push_back(p.a);
+        g_ctx.event_pool.push_back(p.b);
+    }
+    g_ctx.pending.clear();
+}
+
+// Rows of every group of a tree level, summed (= rows touched by one apply).
+static long level_rows(const Tree &t, int level) {
+    if (level == 0) return t.M;
+    long r = 0;
+    const int nprev = t.lv[level - 1].groups;
+    for (int g = 0; g < t.lv[level].groups; ++g) r += (long)std::min(t.F, nprev - g * t.F) * t.bk;
+    return r;
+}
+
+// --------------------------------------------------------------------------
+// stage 1 panel loop on a device matrix
+// --------------------------------------------------------------------------
+template <typename T>
+static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
+    size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
+    need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
+    int rc = ensure_ws(need);
+    if (rc) return rc;
+    TreeWs ws;
+    for (int k = 0; k < n; k += b) {
+        const int bk = std::min(b, n - k);
+        const int mp = m - k;
+        const int n2 = n - k - bk;
+        T *P = A + (long)k * lda + k;
+        // ---- QR of the column panel A[k:m, k:k+bk], left update of A[k:m, k+bk:n]
+        const Tree tq = make_tree(mp, bk);
+        tree_ws_carve(tq, sizeof(T), g_ctx.ws, ws);
+        for (int l = 0; l < tq.nlevels; ++l) {
+            ProfScope ps("s1_factor", 0, 0, s);
+            HIP_TRY(launch_factor<T>(false, P, lda, tq, l, ws, s));
+        }
+        if (n2 <= 0) continue;
+        for (int l = 0; l < tq.nlevels; ++l) {
+            const double rows = (double)level_rows(tq, l);
+            ProfScope ps("s1_apply", 4.0 * bk * rows * n2, 2.0 * rows * n2 * sizeof(T), s);
+            HIP_TRY(launch_apply<T>(false, P + bk, lda, tq, l, n2, ws, s));
+        }
+        // ---- LQ of the row panel A[k:k+bk, k+bk:n] (logical transpose),
+        //      right update of A[k+bk:m, k+bk:n]
+        const Tree tl = make_tree(n2, bk);
+        tree_ws_carve(tl, sizeof(T), g_ctx.ws, ws);
+        T *Q = P + bk;
+        for (int l = 0; l < tl.nlevels; ++l) {
+            ProfScope ps("s1_factor", 0, 0, s);
+            HIP_TRY(launch_factor<T>(true, Q, lda, tl, l, ws, s));
+        }
+        const int m2 = m - k - bk;
+        if (m2 <= 0) continue;
+        for (int l = 0; l < tl.nlevels; ++l) {
+            const double rows = (double)level_rows(tl, l);
+            ProfScope ps("s1_apply", 4.0 * bk * rows * m2, 2.0 * rows * m2 * sizeof(T), s);
+            HIP_TRY(launch_apply<T>(true, Q + (long)bk * lda, lda, tl, l, m2, ws, s));
+        }
+    }
+    return BRD_OK;
+}
+
+// --------------------------------------------------------------------------
+// host/device staging shared by both stages
+// --------------------------------------------------------------------------
+static bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+template <typename T>
+static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags) {
+    std::lock_guard<std::mutex> lk(g_ctx.mu);
+    if (!A) return fail(BRD_EINVAL, "A is NULL");
+    if (n < 1 || m < n) return fail(BRD_EINVAL, "need m >= n >= 1 (m=%d n=%d)", m, n);
+    if (lda < n) return fail(BRD_EINVAL, "lda (%d) < n (%d)", lda, n);
+    if (b < 1 || b > kBmax) return fail(BRD_EINVAL, "band width b=%d outside [1,%d]", b, kBmax);
+    if (ngpus > 1) return fail(BRD_EUNSUPPORTED, "multi-GPU stage 1 goes through the distributed entry points");
+    hipStream_t s = stream();
+    const bool dev = (flags & BRD_DEVICE_PTR) != 0;
+    if (dev && !is_device_ptr(A)) return fail(BRD_EINVAL, "BRD_DEVICE_PTR set but A is not device memory");
+    int rc;
+    if (dev) {
+        rc = ge2band_device<T>(A, m, n, lda, b, s);
+        if (rc == BRD_OK && !(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        T *d = nullptr;
+        if (hipMalloc(&d, sizeof(T) * (size_t)m * n) != hipSuccess)
+            return fail(BRD_ENOMEM, "device matrix allocation failed");
+        HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, m,
+                                 hipMemcpyHostToDevice, s));
+        rc = ge2band_device<T>(d, m, n, n, b, s);
+        if (rc == BRD_OK)
+            HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, m,
+                                     hipMemcpyDeviceToHost, s));
+        hipStreamSynchronize(s);
+        hipFree(d);
+    }
+    if (rc == BRD_OK) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(BRD_EHIP, "stage 1: %s", hipGetErrorString(e));
+    }
+    return rc;
+}
+
+template <typename T>
+static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
+    std::lock_guard<std::mutex> lk(g_ctx.mu);
+    if (!A) return fail(BRD_EINVAL, "A is NULL");
+    if (n < 2) return fail(BRD_EINVAL, "need n >= 2 (n=%d)", n);
+    if (lda < n) return fail(BRD_EINVAL, "lda (%d) < n (%d)", lda, n);
+    if (b < 1 || b > kBmax) return fail(BRD_EINVAL, "band width b=%d outside [1,%d]", b, kBmax);
+    const bool extract = !(flags & BRD_NO_EXTRACT);
+    if (extract && (!dd || !ee)) return fail(BRD_EINVAL, "d/e are NULL (pass BRD_NO_EXTRACT to skip them)");
+    const bool exact = (flags & BRD_EXACT_ORDER) != 0;
+    hipStream_t s = stream();
+    const bool dev = (flags & BRD_DEVICE_PTR) != 0;
+    if (dev) {
+        if (!is_device_ptr(A)) return fail(BRD_EINVAL, "BRD_DEVICE_PTR set but A is not device memory");
+        {
+            ProfScope ps("s2_sweep", 0, 0, s);
+            HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, s));
+        }
+        if (extract) HIP_TRY(launch_extract_bidiag<T>(A, n, lda, dd, ee, s));
+        if (!(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        T *d = nullptr, *de = nullptr;
+        if (hipMalloc(&d, sizeof(T) * ((size_t)n * n + 2 * (size_t)n)) != hipSuccess)
+            return fail(BRD_ENOMEM, "device matrix allocation failed");
+        de = d + (size_t)n * n;
+        HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, n,
+                                 hipMemcpyHostToDevice, s));
+        {
+            ProfScope ps("s2_sweep", 0, 0, s);
+            HIP_TRY(launch_band2bd<T>(d, n, n, b, exact, s));
+        }
+        HIP_TRY(launch_extract_bidiag<T>(d, n, n, de, de + n, s));
+        HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, n,
+                                 hipMemcpyDeviceToHost, s));
+        if (extract) {
+            HIP_TRY(hipMemcpyAsync(dd, de, sizeof(T) * n, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(ee, de + n, sizeof(T) * (n - 1), hipMemcpyDeviceToHost, s));
+        }
+        hipStreamSynchronize(s);
+        hipFree(d);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(BRD_EHIP, "stage 2: %s", hipGetErrorString(e));
+    return BRD_OK;
+}
+
+}  // namespace brd
+
+// ==========================================================================
+// extern "C" entry points
+// ==========================================================================
+extern "C" {
+
+int brd_ge2band_f64(double *A, int m, int n, int lda, int b, int ngpus, unsigned flags) {
+    return brd::ge2band<double>(A, m, n, lda, b, ngpus, flags);
+}
+int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned flags) {
+    return brd::ge2band<float>(A, m, n, lda, b, ngpus, flags);
+}
+int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags) {
+    return brd::band2bd<double>(A, n, lda, b, d, e, flags);
+}
+int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags) {
+    return brd::band2bd<float>(A, n, lda, b, d, e, flags);
+}
+
+int brd_set_stream(void *hip_stream) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    brd::g_ctx.user_stream = (hipStream_t)hip_stream;
+    return BRD_OK;
+}
+
+int brd_profile_enable(int enable) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    brd::g_ctx.prof = enable != 0;
+    return BRD_OK;
+}
+
+int brd_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    brd::prof_drain();
+    brd::g_ctx.acc.clear();
+    return BRD_OK;
+}
+
+int brd_profile_query(const char *kernel, long long *launches, double *total_ms, double *flops,
+                      double *bytes) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    if (!kernel) return brd::fail(BRD_EINVAL, "kernel name is NULL");
+    brd::prof_drain();
+    auto it = brd::g_ctx.acc.find(kernel);
+    brd::ProfAcc a;
+    if (it != brd::g_ctx.acc.end()) a = it->second;
+    if (launches) *launches = a.launches;
+    if (total_ms) *total_ms = a.ms;
+    if (flops) *flops = a.flops;
+    if (bytes) *bytes = a.bytes;
+    return BRD_OK;
+}
+
+int brd_dist_unique_id(void *, int) {
+    return brd::fail(BRD_EUNSUPPORTED, "distributed stage 1 is not built yet");
+}
+int brd_dist_init(int, int, const void *, int) {
+    return brd::fail(BRD_EUNSUPPORTED, "distributed stage 1 is not built yet");
+}
+int brd_dist_finalize(void) { return BRD_OK; }
+
+const char *brd_last_error(void) { return brd::g_err.c_str(); }
+int brd_version(void) { return 1; }
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// Internal declarations shared by the stage-1 / stage-2 HIP translation units
+// and the C-ABI layer (brd_api.cpp).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace brd {
+
+// Largest logical tile (rows) held in LDS by one workgroup.  A Householder
+// tree level groups consecutive rows into chunks of at most kRmax rows
+// (leaf level) or stacks of at most kRmax/bk R-factors (inner levels).
+constexpr int kRmax = 512;
+// Widest panel (= band width b) the kernels support.
+constexpr int kBmax = 32;
+// Column slab width of one apply workgroup.
+constexpr int kSlab = 32;
+
+// One level of the Householder reduction tree of a panel with M logical rows
+// and bk logical columns (see DESIGN.md "Stage 1").
+struct TreeLevel {
+    int level;      // 0 = leaves (chunks of consecutive rows)
+    int groups;     // workgroups at this level
+    int stride;     // leaves per child at this level (F^(level-1)); 1 for level 0
+    int nchild;     // children of the previous level (level >= 1)
+};
+
+struct Tree {
+    int M;          // logical rows of the panel
+    int bk;         // logical columns (reflectors per leaf)
+    int G0;         // leaf chunks
+    int F;          // fan-in of inner levels = kRmax / bk
+    int nlevels;
+    TreeLevel lv[8];
+};
+
+Tree make_tree(int M, int bk);
+
+// Device workspace layout of one tree: per level, per group: V (kRmax x 32),
+// VT (32 x kRmax), T (32 x 32).
+struct TreeWs {
+    void *V[8];
+    void *VT[8];
+    void *T[8];
+};
+size_t tree_ws_bytes(const Tree &t, size_t elem);
+void tree_ws_carve(const Tree &t, size_t elem, void *base, TreeWs &ws);
+
+// Stage-1 launchers (brd_stage1.hip).  view base/ld: logical element (r,c) is
+// base[r*ld + c] (trans = false) or base[c*ld + r] (trans = true).
+template <typename T>
+hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
+                         const TreeWs &ws, hipStream_t s);
+template <typename T>
+hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
+                        int ncols, const TreeWs &ws, hipStream_t s);
+
+// Stage-2 launchers (brd_stage2.hip).
+template <typename T>
+hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, hipStream_t s);
+template <typename T>
+hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStream_t s);
+
+}  // namespace brd

@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: two-stage bidiagonal reduction (dense -> band -> bidiagonal) on
+MI355X, the metric of BASELINE.json:
+    "GFLOP/s for two-stage bidiag reduction, N x N fp64, 1/2/4/8 MI355X"
+counted as 8/3 N^3 flops per matrix (LAPACK GEBRD count).
+
+One step = one full reduction (stage 1 + stage 2) of one synthetic N x N
+matrix, uniform in [0,5) like the reference benchmark (svd_cuda_2.cu:1361),
+already resident in HBM (one pristine copy per step is prepared before the
+timed region, so no copy is timed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192] [--dtype f64] [--band 32]
+
+For N > 1 the driver launches one process per GPU (torch.distributed.run);
+each rank reduces its own matrices (replicas: the sharded stage 1 is not in
+this build, DESIGN.md "Multi-GPU"), the step time is the max over ranks and
+`value` is the aggregate GFLOP/s.
+
+Rank 0 prints ONE JSON line.  Extra fields: the dominant kernel's roofline
+(HIP events around every k_apply launch, on the launch stream) and the CPU
+baseline (the reference's own tiled algorithm, built from its sources by
+oracle/Makefile, timed on a bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "GFLOP/s for two-stage bidiag reduction, N×N fp64, 1/2/4/8 MI355X"
+PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}      # dense MFMA peaks (MI355X_MICROARCH.md / datasheet)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--n", type=int, default=8192)
+    p.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    p.add_argument("--band", type=int, default=32)
+    p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    p.add_argument("--cpu-n", type=int, default=1024)
+    return p.parse_args()
+
+
+def ensure_built():
+    lib = os.path.join(REPO, "svdsolver_amd", "lib", "libbrd_hip.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "svdsolver_amd")], check=True)
+
+
+def cpu_baseline(n: int, band: int) -> dict:
+    """Reference tiled algorithm (parallel::brd_p1 + brd_p2<double>,
+    svd_parallel.h:411/:640) on one n x n fp64 matrix, OpenMP threads =
+    min(16, cores).  Falls back to the single-threaded oracle port."""
+    import ctypes
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from splitmix import uniform_matrix
+    A = uniform_matrix(n, seed=n, lo=0.0, hi=5.0, dtype=np.float64)
+    cores = min(16, os.cpu_count() or 1)
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_fast.so")
+    if os.path.exists(ref):
+        L = ctypes.CDLL(ref)
+        L.ref_set_threads(cores)
+        B = A.copy()
+        t0 = time.perf_counter()
+        L.ref_brd_p1_f64(B.ctypes.data_as(ctypes.c_void_p), n, band)
+        L.ref_brd_p2_f64(B.ctypes.data_as(ctypes.c_void_p), n, band)
+        dt = time.perf_counter() - t0
+        kind, used = "reference", cores
+    else:
+        from oracle import oracle
+        t0 = time.perf_counter()
+        B = oracle.brd_p1(A, band)
+        oracle.brd_p2(B, band)
+        dt = time.perf_counter() - t0
+        kind, used = "port", 1
+    return {"value": round(8.0 / 3.0 * n ** 3 / dt / 1e9, 4), "unit": "GFLOP/s", "cores": used,
+            "kind": kind, "sample": f"one {n}x{n} fp64 two-stage reduction, b={band}, {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    if rank == 0 or world == 1:
+        ensure_built()
+    if world > 1:
+        dist.barrier()
+    import svdsolver_amd as S
+
+    n, b = args.n, args.band
+    tdt = torch.float64 if args.dtype == "f64" else torch.float32
+    nmat = args.warmup + args.steps
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
+    mats = [base.clone() for _ in range(nmat)]
+    del base
+    stream = torch.cuda.current_stream(dev)
+
+    def step(A):
+        S.ge2band(A, b, sync=False)
+        S.band2bd(A, b, sync=False, extract=False)
+
+    for i in range(args.warmup):
+        step(mats[i])
+    torch.cuda.synchronize(dev)
+
+    S.profile_reset()
+    S.profile_enable(True)
+    # stage split on the launch stream (events bracket each stage of every step)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        A = mats[args.warmup + i]
+        ev[i][0].record(stream)
+        S.ge2band(A, b, sync=False)
+        ev[i][1].record(stream)
+        S.band2bd(A, b, sync=False, extract=False)
+        ev[i][2].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    S.profile_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    s1 = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    s2 = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    ap = S.profile_query("s1_apply")
+    fa = S.profile_query("s1_factor")
+    sw = S.profile_query("s2_sweep")
+
+    flops_per = 8.0 / 3.0 * n ** 3
+    value = world * args.steps * flops_per / elapsed / 1e9
+    if rank == 0:
+        ach = ap["flops"] / (ap["ms"] * 1e-3) / 1e12 if ap["ms"] > 0 else 0.0
+        peak = PEAK_TFLOPS[args.dtype]
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic uniform [0,5) N x N, resident in HBM",
+            "config": {"workload": f"two-stage bidiagonal reduction {n}x{n} {args.dtype}, band {b}, "
+                                   f"stage 2 = reference window geometry (compat)",
+                       "n": n, "band": b, "global_batch": world, "parallelism": f"replicas{world}"},
+            "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
+            "roofline": {"kernel": "k_apply (stage-1 trailing update, MFMA)", "bound": "mfma",
+                         "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(ach / peak, 4), "traffic": None,
+                         "launches": ap["launches"],
+                         "avg_launch_us": round(ap["ms"] * 1e3 / max(ap["launches"], 1), 3),
+                         "flops_per_launch": round(ap["flops"] / max(ap["launches"], 1)),
+                         "hbm_gbs_algorithmic": round(ap["bytes"] / (ap["ms"] * 1e-3) / 1e9, 1) if ap["ms"] else 0},
+            "kernel_ms_per_step": {"s1_apply": round(ap["ms"] / args.steps, 3),
+                                   "s1_factor": round(fa["ms"] / args.steps, 3),
+                                   "s2_sweep": round(sw["ms"] / args.steps, 3)},
+        }
+        if args.cpu_baseline == "auto":
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.cpu_n, b)
+            except Exception as e:   # the baseline is reported, never required
+                out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -61,9 +61,11 @@ int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned 
 int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags);
 int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags);
 
-/* Stream used by subsequent calls on this thread's device (hipStream_t; NULL =
- * the library's own stream). */
+/* Stream used by subsequent calls (hipStream_t; NULL = the legacy default
+ * stream).  Until the first call the library uses a stream of its own;
+ * brd_use_own_stream() reverts to it. */
 int brd_set_stream(void *hip_stream);
+int brd_use_own_stream(void);
 
 /* Per-kernel device timing for roofline reporting.  While enabled, the library
  * brackets every launch of the named kernel class with HIP events on the

@@ -35,7 +35,7 @@ BRD_NO_EXTRACT = 0x8
 
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
-    "brd_set_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
+    "brd_set_stream", "brd_use_own_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_finalize", "brd_last_error",
     "brd_version",
 )
@@ -65,6 +65,8 @@ def _load() -> ctypes.CDLL:
         g.restype = ci
     L.brd_set_stream.argtypes = [vp]
     L.brd_set_stream.restype = ci
+    L.brd_use_own_stream.argtypes = []
+    L.brd_use_own_stream.restype = ci
     L.brd_profile_enable.argtypes = [ci]
     L.brd_profile_enable.restype = ci
     L.brd_profile_reset.argtypes = []

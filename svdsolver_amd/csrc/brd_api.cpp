@@ -98,10 +98,14 @@ struct Pending {
 
 struct Ctx {
     std::mutex mu;
+    bool have_user_stream = false;   // true: use user_stream (NULL = legacy default stream)
     hipStream_t user_stream = nullptr;
     hipStream_t own_stream = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0;
+    int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
+    int s2_cap = 0;
+    int *s2_err_host = nullptr;  // pinned copy of the error word
     bool prof = false;
     std::map<std::string, ProfAcc> acc;
     std::vector<Pending> pending;
@@ -110,7 +114,7 @@ struct Ctx {
 static Ctx g_ctx;
 
 static hipStream_t stream() {
-    if (g_ctx.user_stream) return g_ctx.user_stream;
+    if (g_ctx.have_user_stream) return g_ctx.user_stream;
     if (!g_ctx.own_stream) hipStreamCreateWithFlags(&g_ctx.own_stream, hipStreamNonBlocking);
     return g_ctx.own_stream;
 }
@@ -127,6 +131,32 @@ static int ensure_ws(size_t bytes) {
         return fail(BRD_ENOMEM, "workspace allocation of %zu bytes failed", bytes);
     g_ctx.ws_bytes = bytes;
     return BRD_OK;
+}
+
+static int ensure_s2_flags(int n) {
+    if (n + 2 <= g_ctx.s2_cap) return BRD_OK;
+    if (g_ctx.s2_flags) {
+        hipStreamSynchronize(stream());
+        hipFree(g_ctx.s2_flags);
+        g_ctx.s2_flags = nullptr;
+    }
+    if (hipMalloc(&g_ctx.s2_flags, sizeof(int) * (size_t)(n + 2)) != hipSuccess)
+        return fail(BRD_ENOMEM, "stage-2 flag allocation failed");
+    g_ctx.s2_cap = n + 2;
+    if (!g_ctx.s2_err_host && hipHostMalloc(&g_ctx.s2_err_host, sizeof(int)) != hipSuccess)
+        return fail(BRD_ENOMEM, "pinned allocation failed");
+    return BRD_OK;
+}
+
+static int s2_waves() {
+    static int nw = 0;
+    if (!nw) {
+        int dev = 0, cus = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        nw = std::max(64, cus);
+    }
+    return nw;
 }
 
 static hipEvent_t get_event() {
@@ -174,6 +204,25 @@ static void prof_drain() {
         g_ctx.event_pool.push_back(p.b);
     }
     g_ctx.pending.clear();
+}
+
+// Runs the stage-2 sweep on a device matrix; checks the kernel's spin-limit
+// word when the call is synchronous.
+template <typename T>
+static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sync, hipStream_t s) {
+    int rc = ensure_s2_flags(n);
+    if (rc) return rc;
+    int *prog = g_ctx.s2_flags, *err = g_ctx.s2_flags + n + 1;
+    {
+        ProfScope ps("s2_sweep", 0, 0, s);
+        HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, prog, err, s2_waves(), s));
+    }
+    if (sync) {
+        HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, err, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (*g_ctx.s2_err_host) return fail(BRD_EHIP, "stage-2 pipeline stalled (spin limit hit)");
+    }
+    return BRD_OK;
 }
 
 // Rows of every group of a tree level, summed (= rows touched by one apply).
@@ -294,10 +343,8 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
     const bool dev = (flags & BRD_DEVICE_PTR) != 0;
     if (dev) {
         if (!is_device_ptr(A)) return fail(BRD_EINVAL, "BRD_DEVICE_PTR set but A is not device memory");
-        {
-            ProfScope ps("s2_sweep", 0, 0, s);
-            HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, s));
-        }
+        int rc = band2bd_device<T>(A, n, lda, b, exact, !(flags & BRD_ASYNC), s);
+        if (rc) return rc;
         if (extract) HIP_TRY(launch_extract_bidiag<T>(A, n, lda, dd, ee, s));
         if (!(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
     } else {
@@ -307,10 +354,8 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
         de = d + (size_t)n * n;
         HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, n,
                                  hipMemcpyHostToDevice, s));
-        {
-            ProfScope ps("s2_sweep", 0, 0, s);
-            HIP_TRY(launch_band2bd<T>(d, n, n, b, exact, s));
-        }
+        int rc = band2bd_device<T>(d, n, n, b, exact, true, s);
+        if (rc) { hipFree(d); return rc; }
         HIP_TRY(launch_extract_bidiag<T>(d, n, n, de, de + n, s));
         HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, n,
                                  hipMemcpyDeviceToHost, s));
@@ -349,6 +394,13 @@ int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigne
 int brd_set_stream(void *hip_stream) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
     brd::g_ctx.user_stream = (hipStream_t)hip_stream;
+    brd::g_ctx.have_user_stream = true;
+    return BRD_OK;
+}
+
+int brd_use_own_stream(void) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    brd::g_ctx.have_user_stream = false;
     return BRD_OK;
 }
 

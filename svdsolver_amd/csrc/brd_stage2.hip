@@ -20,6 +20,8 @@
 // same code is correct when the sweeps of one launch run on several CUs.
 #include "brd_internal.h"
 
+#include <algorithm>
+
 namespace brd {
 
 template <typename T>
@@ -66,18 +68,23 @@ __device__ __forceinline__ Refl<T> refl_exact(const T *x, int L) {
     return h;
 }
 
-// Per-wave LDS scratch.
-template <typename T>
+// Per-wave LDS scratch.  Fast mode needs only the broadcast vector x; exact
+// mode also holds w, the explicit H (<= 32 x 32) and the lane's row/column.
+template <typename T, bool EXACT>
 struct WaveLds {
+    T x[64];
+};
+template <typename T>
+struct WaveLds<T, true> {
     T x[64];          // reflector source vector (broadcast)
     T w[64];          // reflector (w[0] = 1)
-    T H[32 * 33];     // exact mode: explicit H (L x L, L <= 32... left windows use R <= 32)
-    T buf[64 * 33];   // exact mode: the lane's row/column (dynamic indexing)
+    T H[32 * 33];     // explicit H
+    T buf[64 * 33];   // the lane's row / column (dynamic indexing)
 };
 
 // ---- right window: rows [i1,i2) x cols [j1,j2); reflector from row i1 ------
 template <typename T, bool EXACT>
-__device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T> &S, int lane)
+__device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
 {
     const int R = i2 - i1, L = j2 - j1;   // R <= 64, L <= 32
     T *rowp = A + (long)(i1 + lane) * lda + j1;
@@ -92,7 +99,7 @@ __device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLd
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!EXACT) {
+    if constexpr (!EXACT) {
         const Refl<T> h = refl_fast(S.x, L);
         // w_0 = 1, w_c = x_c * alpha
         T dot = a[0];
@@ -144,7 +151,7 @@ __device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLd
 
 // ---- left window: rows [i1,i2) x cols [j1,j2); reflector from column j1 ----
 template <typename T, bool EXACT>
-__device__ void win_left(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T> &S, int lane)
+__device__ void win_left(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
 {
     const int R = i2 - i1, L = j2 - j1;   // R <= 32, L <= 64
     T *colp = A + (long)i1 * lda + j1 + lane;
@@ -159,7 +166,7 @@ __device__ void win_left(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!EXACT) {
+    if constexpr (!EXACT) {
         const Refl<T> h = refl_fast(S.x, R);
         T dot = a[0];
 #pragma unroll
@@ -252,24 +259,61 @@ struct SweepIter {
     }
 };
 
-// Serial reference order: one wave runs every window of every sweep.
+// Pipelined sweeps.  Sweep i runs on wave i mod NW of a persistent grid and
+// executes its tasks in order; task t of sweep i may start once task t+3 of
+// sweep i-1 has finished (or sweep i-1 is complete).  Lag 3 is the smallest
+// lag for which every pair of overlapping windows keeps the reference's
+// serial order (checked exhaustively over the geometry in
+// tests/test_stage2_schedule.py), so the result equals the serial sweep's --
+// bit for bit in exact-order mode.
+// Hand-off (MI355X_MICROARCH.md, valid forms, table row 1): every band access
+// is an sc1 load/store, the producing wave drains its stores
+// (s_waitcnt vmcnt(0)) before its sc1 progress-flag store, and the consuming
+// wave polls that flag with sc1 loads before its own sc1 loads.
+constexpr int kSpinLimit = 1 << 24;
+
+__device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i) {
+    SweepIter it;
+    it.init(m, n, b, i);
+    return it.ntask;
+}
+
 template <typename T, bool EXACT>
-__global__ void __launch_bounds__(64) k_band2bd_serial(T *A, int m, int n, long lda, int b)
+__global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long lda, int b, int *prog,
+                                                     int *err)
 {
-    __shared__ WaveLds<T> S;
+    __shared__ WaveLds<T, EXACT> S;
     const int lane = threadIdx.x;
-    for (int i = 0; i < n - 1; ++i) {
+    const int nw = gridDim.x;
+    for (int i = blockIdx.x; i < n - 1; i += nw) {
         SweepIter it;
         it.init(m, n, b, i);
+        const int prev_ntask = i > 0 ? sweep_ntask(m, n, b, i - 1) : 0;
         for (int t = 0; t < it.ntask; ++t) {
             bool right;
             const Win wnd = it.task(t, right);
-            if (wnd.j2 <= wnd.j1 || wnd.i2 <= wnd.i1) continue;
-            if (right) win_right<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
-            else       win_left<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
-            // the next window's loads must observe this window's stores
-            __builtin_amdgcn_s_waitcnt(0);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            if (i > 0) {
+                const int need = min(t + 4, prev_ntask);
+                if (lane == 0) {
+                    int spins = 0;
+                    while (__hip_atomic_load(prog + i - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) {
+                            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (wnd.j2 > wnd.j1 && wnd.i2 > wnd.i1) {
+                if (right) win_right<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
+                else       win_left<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (lane == 0) __hip_atomic_store(prog + i, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -282,13 +326,20 @@ __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
     if (i < n - 1) e[i] = A[(long)i * lda + i + 1];
 }
 
+// prog: n ints, err: 1 int (device workspace, zeroed here).
 template <typename T>
-hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, hipStream_t s)
+hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *prog, int *err,
+                          int nwaves, hipStream_t s)
 {
+    hipError_t e = hipMemsetAsync(prog, 0, sizeof(int) * (size_t)(n + 1), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(err, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    const int grid = std::max(1, std::min(nwaves, n - 1));
     if (exact_order)
-        hipLaunchKernelGGL((k_band2bd_serial<T, true>), dim3(1), dim3(64), 0, s, A, n, n, lda, b);
+        hipLaunchKernelGGL((k_band2bd_pipe<T, true>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, prog, err);
     else
-        hipLaunchKernelGGL((k_band2bd_serial<T, false>), dim3(1), dim3(64), 0, s, A, n, n, lda, b);
+        hipLaunchKernelGGL((k_band2bd_pipe<T, false>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, prog, err);
     return hipGetLastError();
 }
 
@@ -299,8 +350,8 @@ hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStr
     return hipGetLastError();
 }
 
-template hipError_t launch_band2bd<double>(double *, int, long, int, bool, hipStream_t);
-template hipError_t launch_band2bd<float>(float *, int, long, int, bool, hipStream_t);
+template hipError_t launch_band2bd<double>(double *, int, long, int, bool, int *, int *, int, hipStream_t);
+template hipError_t launch_band2bd<float>(float *, int, long, int, bool, int *, int *, int, hipStream_t);
 template hipError_t launch_extract_bidiag<double>(const double *, int, long, double *, double *, hipStream_t);
 template hipError_t launch_extract_bidiag<float>(const float *, int, long, float *, float *, hipStream_t);
 

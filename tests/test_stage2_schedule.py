@@ -1,0 +1,71 @@
+"""The stage-2 pipeline's lag-3 rule preserves the reference's serial order.
+
+Task t of sweep i may start once task t+3 of sweep i-1 is done
+(brd_stage2.hip, k_band2bd_pipe).  This holds iff every pair of overlapping
+windows (i, t), (i', t') with i < i' satisfies t <= t' + 3 (i' - i).  The
+windows are enumerated exactly as the reference's brd_p2 builds them
+(svd_parallel.h:648-688), including clipped and empty ones.
+"""
+import pytest
+
+
+def windows(m, n, b):
+    bs = b + 1
+    W = {}
+    for i in range(n - 1):
+        tl = (i, min(i + bs, m), i + 1, min(i + bs, n))
+        tasks = [tl]
+        tl = (i + 1, min(i + bs, m), i + 1, min(i + 2 * bs - 1, n))
+        tasks.append(tl)
+        nbtx = (n - tl[3]) // (bs - 1)
+        for _ in range(nbtx + 1):
+            end_i = min(tl[1] + bs - 1, m)
+            sj = min(tl[2] + bs - 1, n)
+            ej3 = min(tl[3] + bs - 1, n)
+            tr = (tl[0], end_i, sj, tl[3])
+            tl = (tl[1], end_i, sj, ej3)
+            tasks += [tr, tl]
+        W[i] = [t if (t[3] > t[2] and t[1] > t[0]) else None for t in tasks]
+    return W
+
+
+def _overlap(a, b):
+    return a[0] < b[1] and b[0] < a[1] and a[2] < b[3] and b[2] < a[3]
+
+
+def worst_slack(n, b, lag):
+    W = windows(n, n, b)
+    worst = -10 ** 9
+    for i in W:
+        for ip in range(i + 1, min(n - 1, i + 2 * b + 4)):
+            for t, wa in enumerate(W[i]):
+                if wa is None:
+                    continue
+                for tp, wb in enumerate(W[ip]):
+                    if wb is not None and _overlap(wa, wb):
+                        worst = max(worst, t - tp - lag * (ip - i))
+    return worst
+
+
+@pytest.mark.parametrize("n,b", [(64, 4), (100, 4), (130, 8), (128, 32), (257, 32), (300, 16), (50, 2), (40, 1)])
+def test_lag3_preserves_serial_order(n, b):
+    assert worst_slack(n, b, 3) <= 0
+
+
+@pytest.mark.parametrize("n,b", [(64, 4), (128, 32)])
+def test_lag2_is_not_enough(n, b):
+    assert worst_slack(n, b, 2) > 0
+
+
+def test_windows_fit_kernel_limits():
+    """Right windows <= 2b x b, left windows <= b x 2b (one row/column per lane)."""
+    for n, b in [(257, 32), (100, 4), (64, 1)]:
+        for i, tasks in windows(n, n, b).items():
+            for t, w in enumerate(tasks):
+                if w is None:
+                    continue
+                rows, cols = w[1] - w[0], w[3] - w[2]
+                if t % 2 == 0:
+                    assert rows <= max(2 * b, b + 1) and cols <= b
+                else:
+                    assert rows <= b and cols <= 2 * b

@@ -1,0 +1,147 @@
+// svd_gpu -- command-line front end with the reference's grammar
+// (svd_cuda_2.cu:1251-1258, :1296-1434; README.md:77-83), on the MI355X library.
+//
+//   svd_gpu check <64|512|1024> [--dtype f32|f64] [--data-dir DIR]
+//       Reads test_<T>_<N>_<N>.bin, runs stage 1 with band 4 (the reference's
+//       check band, svd_cuda_2.cu:1300) and stage 2, and prints the reference's
+//       band metric (Matrix::mse, matrix_gpu.h:438) against band_<T>_<N>_<N>.bin
+//       and bidiagonal_<T>_<N>_<N>.bin when those fixtures are present.
+//       Unlike the reference, stage 2 is the band->bidiagonal sweep whose output
+//       the bidiagonal fixtures hold (the reference's check runs a one-stage GK
+//       reduction there and never matches them).
+//   svd_gpu benchmark <step> <nsteps> <ninst> <b> [--dtype f32|f64] [--csv PATH]
+//       N = k*step for k = 1..nsteps, ninst matrices uniform in [0,5) each;
+//       prints "N = <n> | <sec> sec" per size and writes the reference's 2-row
+//       CSV (N row, stage-1 seconds row) plus a third row with stage-2 seconds.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "brd.h"
+#include "brd_matrix.hpp"
+
+namespace {
+
+template <typename T> int ge2band(T *A, int n, int b);
+template <> int ge2band<double>(double *A, int n, int b) { return brd_ge2band_f64(A, n, n, n, b, 1, 0); }
+template <> int ge2band<float>(float *A, int n, int b) { return brd_ge2band_f32(A, n, n, n, b, 1, 0); }
+template <typename T> int band2bd(T *A, int n, int b, T *d, T *e);
+template <> int band2bd<double>(double *A, int n, int b, double *d, double *e) { return brd_band2bd_f64(A, n, n, b, d, e, 0); }
+template <> int band2bd<float>(float *A, int n, int b, float *d, float *e) { return brd_band2bd_f32(A, n, n, b, d, e, 0); }
+
+void die(const char *what, int rc) {
+    std::fprintf(stderr, "%s failed (%d): %s\n", what, rc, brd_last_error());
+    std::exit(1);
+}
+
+template <typename T>
+int check(int n, const std::string &dir, const char *tname) {
+    const int band = 4;
+    const std::string sz = std::to_string(n) + "_" + std::to_string(n) + ".bin";
+    brd::Matrix<T> A(n, n);
+    const std::string in = dir + "/test_" + tname + "_" + sz;
+    std::printf("Reading file: %s\n", in.c_str());
+    if (!A.read(in)) { std::fprintf(stderr, "cannot read %s\n", in.c_str()); return 1; }
+    A.print();
+    int rc = ge2band<T>(A.data(), n, band);
+    if (rc) die("brd_ge2band", rc);
+    std::printf("\n\nMI355X Test (Band):\n");
+    A.print(16);
+    brd::Matrix<T> ref(n, n);
+    if (ref.read(dir + "/band_" + tname + "_" + sz))
+        std::printf("\n\nMSE of Band Reduction: %.9g\n", A.mse(ref, band));
+    else
+        std::printf("\n\nband fixture not found; MSE of Band Reduction not computed\n");
+    std::vector<T> d(n), e(n > 1 ? n - 1 : 1);
+    rc = band2bd<T>(A.data(), n, band, d.data(), e.data());
+    if (rc) die("brd_band2bd", rc);
+    std::printf("\n\nMI355X Test (Bidiagonal):\n");
+    A.print(10);
+    if (ref.read(dir + "/bidiagonal_" + tname + "_" + sz))
+        std::printf("\n\nMSE of Bidiagonal Reduction: %.9g\n", A.mse(ref, 2));
+    else
+        std::printf("\n\nbidiagonal fixture not found; MSE of Bidiagonal Reduction not computed\n");
+    return 0;
+}
+
+template <typename T>
+int benchmark(int step, int nsteps, int ninst, int b, const std::string &csv) {
+    std::printf("Benchmark: MI355X two-stage bidiagonal reduction (%s)\n", sizeof(T) == 8 ? "fp64" : "fp32");
+    std::printf("\tBand size: %d\n\tStep size: %d\n\tNumber of steps: %d\n\tNumber of test instances: %d\n", b, step,
+                nsteps, ninst);
+    std::vector<int> xs;
+    std::vector<double> y1, y2;
+    for (int k = 1; k <= nsteps; ++k) {
+        const int n = k * step;
+        double t1 = 0, t2 = 0;
+        for (int r = 0; r < ninst; ++r) {
+            brd::Matrix<T> A(n, n);
+            A.fill(T(0), T(5), 1000003ull * n + r);
+            std::vector<T> d(n), e(n);
+            auto a = std::chrono::steady_clock::now();
+            int rc = ge2band<T>(A.data(), n, b);
+            if (rc) die("brd_ge2band", rc);
+            auto m = std::chrono::steady_clock::now();
+            rc = band2bd<T>(A.data(), n, b, d.data(), e.data());
+            if (rc) die("brd_band2bd", rc);
+            auto z = std::chrono::steady_clock::now();
+            t1 += std::chrono::duration<double>(m - a).count();
+            t2 += std::chrono::duration<double>(z - m).count();
+        }
+        t1 /= ninst;
+        t2 /= ninst;
+        const double gf = 8.0 / 3.0 * (double)n * n * n / (t1 + t2) / 1e9;
+        std::printf("N = %d | %g sec (dense -> band) | %g sec (band -> bidiagonal) | %.2f GFLOP/s (host buffers, "
+                    "PCIe included)\n", n, t1, t2, gf);
+        xs.push_back(n);
+        y1.push_back(t1);
+        y2.push_back(t2);
+    }
+    std::ofstream f(csv);
+    for (size_t i = 0; i < xs.size(); ++i) f << xs[i] << (i + 1 < xs.size() ? ", " : "\n");
+    for (size_t i = 0; i < y1.size(); ++i) f << y1[i] << (i + 1 < y1.size() ? ", " : "\n");
+    for (size_t i = 0; i < y2.size(); ++i) f << y2[i] << (i + 1 < y2.size() ? ", " : "\n");
+    std::printf("Writing results to file ... %s\n", csv.c_str());
+    return 0;
+}
+
+void help() {
+    std::printf("Options for MI355X two-stage bidiagonal reduction\n"
+                "\n(1) Run benchmark tests.\n"
+                "\t>> benchmark [<int> Step size] [<int> Number of steps] [<int> Number of test instances] "
+                "[<int> Band size] [--dtype f32|f64] [--csv PATH]\n"
+                "\tExample: ./svd_gpu benchmark 1024 4 1 32\n"
+                "\n(2) Correctness test against the reference fixtures (band size 4).\n"
+                "\t>> check [64|512|1024] [--dtype f32|f64] [--data-dir DIR]\n"
+                "\tExample: ./svd_gpu check 64\n");
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    std::string dtype = "f32", dir = getenv("BRD_DATA_DIR") ? getenv("BRD_DATA_DIR") : "data",
+                csv = "data/cuda_2_benchmark.csv";
+    std::vector<std::string> pos;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "--dtype" && i + 1 < argc) dtype = argv[++i];
+        else if (a == "--data-dir" && i + 1 < argc) dir = argv[++i];
+        else if (a == "--csv" && i + 1 < argc) csv = argv[++i];
+        else pos.push_back(a);
+    }
+    if (pos.size() >= 2 && pos[0] == "check") {
+        const int n = std::atoi(pos[1].c_str());
+        return dtype == "f64" ? check<double>(n, dir, "double") : check<float>(n, dir, "float");
+    }
+    if (pos.size() >= 5 && pos[0] == "benchmark") {
+        const int step = std::atoi(pos[1].c_str()), ns = std::atoi(pos[2].c_str()), ni = std::atoi(pos[3].c_str()),
+                  b = std::atoi(pos[4].c_str());
+        return dtype == "f64" ? benchmark<double>(step, ns, ni, b, csv) : benchmark<float>(step, ns, ni, b, csv);
+    }
+    help();
+    return 0;
+}

@@ -15,8 +15,6 @@ namespace brd {
 constexpr int kRmax = 512;
 // Widest panel (= band width b) the kernels support.
 constexpr int kBmax = 32;
-// Column slab width of one apply workgroup.
-constexpr int kSlab = 32;
 
 // One level of the Householder reduction tree of a panel with M logical rows
 // and bk logical columns (see DESIGN.md "Stage 1").

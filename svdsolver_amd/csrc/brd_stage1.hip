@@ -119,21 +119,14 @@ constexpr int kRG = kFT / 32;    // row groups
 constexpr int kQ = kRmax / kRG;  // rows per thread
 constexpr int kFS = 33;          // LDS row stride of the staging tile
 
-// Register-array access with a wave-uniform index (a scalar branch, not a
-// select chain or scratch).
+// Row j < 32 of the tile lives in register slot j / kRG, i.e. slot 0 or 1:
+// two-way selects keep every register index static (no scratch).
+static_assert(kRG >= 16, "row j < 32 must live in register slot 0 or 1");
 template <typename T, int N>
-__device__ __forceinline__ T reg_get(const T (&x)[N], int q) {
-    T v = (T)0;
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-        if (k == q) v = x[k];
-    return v;
-}
+__device__ __forceinline__ T slot01_get(const T (&x)[N], int q) { return q == 0 ? x[0] : x[1]; }
 template <typename T, int N>
-__device__ __forceinline__ void reg_set(T (&x)[N], int q, T v) {
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-        if (k == q) x[k] = v;
+__device__ __forceinline__ void slot01_set(T (&x)[N], int q, T v) {
+    if (q == 0) x[0] = v; else x[1] = v;
 }
 
 template <typename T, bool TR>
@@ -163,7 +156,7 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
         (&sZ[0][0])[e] = (T)0;
         (&sT[0][0])[e] = (T)0;
     }
-    if (tid < 32) { sU1[tid] = (T)1; sTau[tid] = (T)0; }
+    if (tid < 32) { sU1[tid] = (T)1; sTau[tid] = (T)0; }   // sU1: 1/u1 per column
     __syncthreads();
 
     // ---- stage the tile into registers ------------------------------------
@@ -216,30 +209,30 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
         }
         wave_sync();
         // (1) partial G_c = sum_{i>j} X[i][j] X[i][c] over this thread's rows
-        T p = (T)0;
+        //     (four independent chains)
+        T p4[4] = {(T)0, (T)0, (T)0, (T)0};
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             colj[q] = sColj[rg + kRG * q];
-            p = fma(colj[q], xr[q], p);
+            p4[q & 3] = fma(colj[q], xr[q], p4[q & 3]);
         }
+        T p = (p4[0] + p4[1]) + (p4[2] + p4[3]);
         p += __shfl_xor(p, 32);
         if ((lane >> 5) == 0) sRed[pb][w][c] = p;
-        if (rg == jr) sRow[pb][c] = reg_get(xr, jq);
+        if (rg == jr) sRow[pb][c] = slot01_get(xr, jq);
         __syncthreads();
-        // T column j-1 (lanes 0..31 of wave 0; v_c^T v_{j-1} is in sZ since step j-1)
-        if (tid < 32 && j > 0) {
-            const int a = tid, jj = j - 1;
-            T s = (T)0;
-            for (int cc = 0; cc < jj; ++cc) s = fma(sT[a][cc], sZ[cc][jj], s);
-            const T tj = sTau[jj];
-            sT[a][jj] = a < jj ? -tj * s : (a == jj ? tj : (T)0);
-        }
         // (2) reflector (LAPACK-style: tau = 0 when the sub-column is zero)
-        T Gc = (T)0, Gj = (T)0;
+        T Gc, Gj;
+        {
+            T gc[kFT / 64], gj[kFT / 64];
 #pragma unroll
-        for (int ww = 0; ww < kFT / 64; ++ww) {
-            Gc += sRed[pb][ww][c];
-            Gj += sRed[pb][ww][j];
+            for (int ww = 0; ww < kFT / 64; ++ww) { gc[ww] = sRed[pb][ww][c]; gj[ww] = sRed[pb][ww][j]; }
+#pragma unroll
+            for (int h = kFT / 128; h >= 1; h >>= 1)
+#pragma unroll
+                for (int ww = 0; ww < h; ++ww) { gc[ww] += gc[ww + h]; gj[ww] += gj[ww + h]; }
+            Gc = gc[0];
+            Gj = gj[0];
         }
         const T x0 = sRow[pb][j];
         T alpha = x0, u1 = (T)1, tau = (T)0;
@@ -256,32 +249,41 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
             const T tw = tau * wc, twu = tw * inv_u1;
 #pragma unroll
             for (int q = 0; q < kQ; ++q) xr[q] = fma(-twu, colj[q], xr[q]);   // rows i > j
-            if (rg == jr) reg_set(xr, jq, reg_get(xr, jq) - tw);               // row j (v_j = 1)
+            if (rg == jr) slot01_set(xr, jq, slot01_get(xr, jq) - tw);         // row j (v_j = 1)
         } else if (c == j) {
-            if (rg == jr) reg_set(xr, jq, alpha);
-            if (rg == 0) { sU1[j] = u1; sTau[j] = tau; }
+            if (rg == jr) slot01_set(xr, jq, alpha);
+            if (rg == 0) { sU1[j] = inv_u1; sTau[j] = tau; }
         } else if (c < j && rg == 0) {
-            sZ[c][j] = wc / sU1[c];                      // v_c^T v_j
+            sZ[c][j] = wc * sU1[c];                      // v_c^T v_j  (sU1 holds 1/u1)
         }
     }
     __syncthreads();
     STAMP(4);
 
-    // ---- last column of T ---------------------------------------------------
+    // ---- T (LAPACK larft): T[:, j] = -tau_j T[:, :j] (V^T v_j)[:j], T[j][j] = tau_j
+    // Lane a of wave 0 keeps row a of T in registers (fully unrolled, static
+    // indices); z = V^T V (strict upper part) is read from sZ as broadcasts.
     T *Tm = Tws + (size_t)grp * 32 * 32;
-    if (tid < 32 && kk > 0) {
-        const int a = tid, jj = kk - 1;
-        T s = (T)0;
-        for (int cc = 0; cc < jj; ++cc) s = fma(sT[a][cc], sZ[cc][jj], s);
-        const T tj = sTau[jj];
-        sT[a][jj] = a < jj ? -tj * s : (a == jj ? tj : (T)0);
+    if (tid < 32) {
+        const int a = tid;
+        T trow[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            T s = (T)0;
+#pragma unroll
+            for (int cc = 0; cc < j; ++cc) s = fma(trow[cc], sZ[cc][j], s);
+            const T tj = j < kk ? sTau[j] : (T)0;
+            trow[j] = a < j ? -tj * s : (a == j ? tj : (T)0);
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) sT[a][j] = trow[j];
     }
     STAMP(5);
     // ---- outputs ------------------------------------------------------------
     T *V = Vws + (size_t)grp * kRmax * 32;
     T *VT = VTws + (size_t)grp * 32 * kRmax;
     const int nrp = (nr + 15) & ~15;
-    const T iu = (T)1 / sU1[c];
+    const T iu = sU1[c];
     // V (kRmax x 32, row-major, rows < nrp) from registers; scaled copy to LDS for VT
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {

@@ -16,13 +16,54 @@
 //                in its operation order with fp contraction off -- the output
 //                is bit-identical to the reference's CPU code on the same
 //                input (used to pin the geometry in tests).
-// Band data are read and written with agent-coherent (sc1) accesses, so the
-// same code is correct when the sweeps of one launch run on several CUs.
+//
+// Two schedules (DESIGN.md "Stage 2"):
+//   k_band2bd_bundle  (default) bundles of S consecutive sweeps per workgroup,
+//                     one wave per sweep, the active band rows in an LDS ring
+//                     filled / drained by an IO wave; bundles hand rows to the
+//                     next bundle through HBM.
+//   k_band2bd_pipe    one wave per sweep straight on HBM (sc1 hand-offs).
 #include "brd_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace brd {
+
+#ifdef BRD_STAMPS
+// Debug build only: per-bundle timeline (s_memtime) of k_band2bd_bundle:
+// [0] bundle start, [1] leading sweep task 0 done, [2] leading sweep done,
+// [3] trailing sweep done, [4] writer done, [5] loader done.
+constexpr int kS2Stamp = 6, kS2MaxBundles = 4096;
+__device__ unsigned long long g_s2stamps[kS2MaxBundles * kS2Stamp];
+#define S2STAMP(beta, k)                                                         \
+    do {                                                                         \
+        if ((beta) < kS2MaxBundles) g_s2stamps[(beta) * kS2Stamp + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+// Per-bundle cycle accounting: [wave*3 + {0: wait prev sweep, 1: wait rows, 2: work}]
+// for compute waves 0..2, then loader {9: wait prev bundle, 10: wait ring, 11: load},
+// writer {12: wait fronts, 13: write}.
+constexpr int kS2Acc = 16;
+__device__ unsigned long long g_s2acc[kS2MaxBundles * kS2Acc];
+hipError_t read_s2stamps(unsigned long long *out, size_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2stamps), sizeof(unsigned long long) * n);
+}
+hipError_t read_s2acc(unsigned long long *out, size_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2acc), sizeof(unsigned long long) * n);
+}
+#define S2T0() const unsigned long long _t0 = __builtin_amdgcn_s_memtime()
+#define S2T(var) var = __builtin_amdgcn_s_memtime()
+#define S2ACC(beta, k, t0, t1) \
+    do { if ((beta) < kS2MaxBundles && lane == 0) g_s2acc[(beta) * kS2Acc + (k)] += (t1) - (t0); } while (0)
+#else
+#define S2STAMP(beta, k) do {} while (0)
+#define S2ACC(beta, k, t0, t1) do {} while (0)
+#endif
+#ifdef BRD_STAMPS
+#define S2CLK() __builtin_amdgcn_s_memtime()
+#else
+#define S2CLK() 0ull
+#endif
 
 template <typename T>
 __device__ __forceinline__ T ld_c(const T *p) {
@@ -33,6 +74,12 @@ __device__ __forceinline__ void st_c(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void wave_sync2() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Reflector of csc586::serial::householder (svd_serial.h:189-218), including
 // its mixed precision (s, u1 and tau are doubles, rounded to T).
 template <typename T>
@@ -41,26 +88,31 @@ struct Refl {
     T tau;
 };
 
-template <typename T>
-__device__ __forceinline__ Refl<T> refl_fast(const T *x, int L) {
+// Reflector of the vector held in the calling lane's registers (lane 0 holds
+// the window's first row / column), computed in the reference's operation order
+// in exact mode (fp contraction off).
+template <typename T, bool EXACT>
+__device__ __forceinline__ Refl<T> refl_regs(const T (&x)[32], int L) {
     T acc = (T)0;
-    for (int r = 0; r < L; ++r) acc = fma(x[r], x[r], acc);
-    const T nrm = sqrt(acc);
-    const double s = x[0] >= (T)0 ? -1.0 : 1.0;   // -copysign(1, x0) (x0 = -0 -> treated as +0)
-    const double u1 = (double)x[0] - s * (double)nrm;
-    Refl<T> h;
-    h.alpha = (T)(1. / u1);
-    h.tau = (T)(-s * u1 / (double)nrm);
-    return h;
-}
-
-template <typename T>
-__device__ __forceinline__ Refl<T> refl_exact(const T *x, int L) {
+    double s;
+    T nrm;
+    if constexpr (EXACT) {
 #pragma clang fp contract(off)
-    T acc = (T)0;
-    for (int r = 0; r < L; ++r) acc = acc + x[r] * x[r];
-    const T nrm = (T)sqrt((double)acc);
-    const double s = -copysign(1.0, (double)x[0]);
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+            if (r < L) acc = acc + x[r] * x[r];
+        nrm = (T)sqrt((double)acc);
+        s = -copysign(1.0, (double)x[0]);
+    } else {
+        T acc1 = (T)0;   // two chains: fast mode does not keep the serial order
+#pragma unroll
+        for (int r = 0; r < 32; r += 2) {
+            if (r < L) acc = fma(x[r], x[r], acc);
+            if (r + 1 < L) acc1 = fma(x[r + 1], x[r + 1], acc1);
+        }
+        nrm = sqrt(acc + acc1);
+        s = x[0] >= (T)0 ? -1.0 : 1.0;   // -copysign(1, x0) (x0 = -0 -> treated as +0)
+    }
     const double u1 = (double)x[0] - s * (double)nrm;
     Refl<T> h;
     h.alpha = (T)(1. / u1);
@@ -68,57 +120,101 @@ __device__ __forceinline__ Refl<T> refl_exact(const T *x, int L) {
     return h;
 }
 
-// Per-wave LDS scratch.  Fast mode needs only the broadcast vector x; exact
-// mode also holds w, the explicit H (<= 32 x 32) and the lane's row/column.
+// Per-wave LDS scratch.  Fast mode needs only the broadcast reflector w and
+// tau; exact mode also holds x, the explicit H (<= 32 x 32) and the lane's
+// row/column.
 template <typename T, bool EXACT>
 struct WaveLds {
-    T x[64];
+    T w[64];
+    T h[2];
 };
 template <typename T>
 struct WaveLds<T, true> {
-    T x[64];          // reflector source vector (broadcast)
     T w[64];          // reflector (w[0] = 1)
+    T h[2];           // alpha, tau
+    T x[64];          // reflector source vector
     T H[32 * 33];     // explicit H
     T buf[64 * 33];   // the lane's row / column (dynamic indexing)
 };
 
-// ---- right window: rows [i1,i2) x cols [j1,j2); reflector from row i1 ------
+// Element accessors: the band in HBM (agent-coherent sc1 accesses) or a ring
+// of band rows in LDS.  row(r) returns a pointer p with p[c] = element (r, c).
+template <typename T>
+struct HbmAcc {
+    T *A;
+    long lda;
+    __device__ __forceinline__ T *row(int r) const { return A + (long)r * lda; }
+    __device__ __forceinline__ T ld(const T *p) const { return ld_c(p); }
+    __device__ __forceinline__ void st(T *p, T v) const { st_c(p, v); }
+};
+// r mod R without an integer division: with magic = ceil(2^32 / R),
+// umulhi(r, magic) = floor(r / R) exactly for 0 <= r < 2^32 / R (the rounding
+// excess r * (magic - 2^32/R) / 2^32 stays below 1/R); the compare is a guard.
+__device__ __forceinline__ int fast_mod(int r, int R, unsigned magic) {
+    int s = r - (int)__umulhi((unsigned)r, magic) * R;
+    return s >= R ? s - R : s;
+}
+
+template <typename T>
+struct RingAcc {
+    T *d;            // ring rows * P elements
+    int P;           // row pitch ring_pitch(b) >= 3b - 1 (diagonals -(b-1) .. 2b-1)
+    int R;           // ring rows
+    int off;         // b - 1
+    unsigned magic;  // ceil(2^32 / R)
+    __device__ __forceinline__ int slot(int r) const { return fast_mod(r, R, magic); }
+    __device__ __forceinline__ T *row(int r) const { return d + slot(r) * P + off - r; }
+    __device__ __forceinline__ T ld(const T *p) const { return *p; }
+    __device__ __forceinline__ void st(T *p, T v) const { *p = v; }
+};
+
+// Apply the reflector of lane 0's vector to every lane's vector a[0..L) (a
+// right window's row or a left window's column).  Lane 0 forms the reflector
+// from its registers and broadcasts w (and tau) through LDS once.
 template <typename T, bool EXACT>
-__device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
+__device__ __forceinline__ void refl_apply(T (&a)[32], int L, WaveLds<T, EXACT> &S, int lane, bool row_major)
 {
-    const int R = i2 - i1, L = j2 - j1;   // R <= 64, L <= 32
-    T *rowp = A + (long)(i1 + lane) * lda + j1;
-    T a[32];
-#pragma unroll
-    for (int c = 0; c < 32; ++c) a[c] = (lane < R && c < L) ? ld_c(rowp + c) : (T)0;
-    if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < 32; ++c)
-            if (c < L) S.x[c] = a[c];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if constexpr (!EXACT) {
-        const Refl<T> h = refl_fast(S.x, L);
-        // w_0 = 1, w_c = x_c * alpha
-        T dot = a[0];
+        if (lane == 0) {
+            const Refl<T> h = refl_regs<T, false>(a, L);
+            S.h[1] = h.tau;
 #pragma unroll
-        for (int c = 1; c < 32; ++c)
-            if (c < L) dot = fma(a[c], S.x[c] * h.alpha, dot);
-        const T td = h.tau * dot;
+            for (int c = 1; c < 32; ++c)
+                if (c < L) S.w[c] = a[c] * h.alpha;   // w_0 = 1, w_c = x_c * alpha
+        }
+        wave_sync2();
+        const T tau = S.h[1];
+        T w[32];
+#pragma unroll
+        for (int c = 1; c < 32; ++c) w[c] = c < L ? S.w[c] : (T)0;
+        T d0 = a[0], d1 = (T)0, d2 = (T)0, d3 = (T)0;
+#pragma unroll
+        for (int c = 1; c < 32; c += 4) {
+            d1 = fma(a[c], w[c], d1);
+            if (c + 1 < 32) d2 = fma(a[c + 1], w[c + 1], d2);
+            if (c + 2 < 32) d3 = fma(a[c + 2], w[c + 2], d3);
+            if (c + 3 < 32) d0 = fma(a[c + 3], w[c + 3], d0);
+        }
+        const T td = tau * ((d0 + d1) + (d2 + d3));
         a[0] -= td;
 #pragma unroll
         for (int c = 1; c < 32; ++c)
-            if (c < L) a[c] = fma(-td, S.x[c] * h.alpha, a[c]);
+            if (c < L) a[c] = fma(-td, w[c], a[c]);
     } else {
 #pragma clang fp contract(off)
-        const Refl<T> h = refl_exact(S.x, L);
-        // w and explicit H (svd_serial.h:203-214), one entry per lane at a time
+        if (lane == 0) {
+            const Refl<T> h = refl_regs<T, true>(a, L);
+            S.h[0] = h.alpha;
+            S.h[1] = h.tau;
+#pragma unroll
+            for (int c = 0; c < 32; ++c)
+                if (c < L) S.x[c] = a[c];
+        }
+        wave_sync2();
+        const Refl<T> h{S.h[0], S.h[1]};
+        // w and explicit H (svd_serial.h:203-214)
         for (int c = lane; c < L; c += 64) S.w[c] = (c == 0) ? (T)1. : S.x[c] * h.alpha;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync2();
         const T mt = -h.tau;
         for (int e = lane; e < L * L; e += 64) {
             const int k = e / L, c = e - k * L;
@@ -130,87 +226,137 @@ __device__ void win_right(T *A, long lda, int i1, int i2, int j1, int j2, WaveLd
 #pragma unroll
         for (int c = 0; c < 32; ++c)
             if (c < L) my[c] = a[c];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // A_t <- A_t H : out[c] = sum_k a[k] H[k][c]   (matrix.h:234 order)
+        wave_sync2();
+        // right window: A_t <- A_t H, out[c] = sum_k a[k] H[k][c]  (matrix.h:234 order)
+        // left window:  A_t <- H A_t, out[r] = sum_k H[r][k] a[k]
         for (int c = 0; c < L; ++c) {
             T acc = (T)0;
-            for (int k = 0; k < L; ++k) acc += my[k] * S.H[k * 33 + c];
+            if (row_major)
+                for (int k = 0; k < L; ++k) acc += my[k] * S.H[k * 33 + c];
+            else
+                for (int k = 0; k < L; ++k) acc += S.H[c * 33 + k] * my[k];
 #pragma unroll
             for (int cc = 0; cc < 32; ++cc)
                 if (cc == c) a[cc] = acc;
         }
     }
+}
+
+// ---- right window: rows [i1,i2) x cols [j1,j2); reflector from row i1 ------
+template <typename T, bool EXACT, typename Acc>
+__device__ void win_right(const Acc &A, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
+{
+    const int R = i2 - i1, L = j2 - j1;   // R <= 64, L <= 32
+    T *rowp = A.row(i1 + (lane < R ? lane : 0)) + j1;
+    T a[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) a[c] = (lane < R && c < L) ? A.ld(rowp + c) : (T)0;
+    refl_apply<T, EXACT>(a, L, S, lane, true);
     if (lane < R) {
 #pragma unroll
         for (int c = 0; c < 32; ++c)
-            if (c < L) st_c(rowp + c, a[c]);
+            if (c < L) A.st(rowp + c, a[c]);
     }
 }
 
 // ---- left window: rows [i1,i2) x cols [j1,j2); reflector from column j1 ----
-template <typename T, bool EXACT>
-__device__ void win_left(T *A, long lda, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
+template <typename T, bool EXACT, typename Acc>
+__device__ void win_left(const Acc &A, int i1, int i2, int j1, int j2, WaveLds<T, EXACT> &S, int lane)
 {
     const int R = i2 - i1, L = j2 - j1;   // R <= 32, L <= 64
-    T *colp = A + (long)i1 * lda + j1 + lane;
+    const int col = j1 + (lane < L ? lane : 0);
     T a[32];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) a[r] = (lane < L && r < R) ? ld_c(colp + (long)r * lda) : (T)0;
-    if (lane == 0) {
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-            if (r < R) S.x[r] = a[r];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if constexpr (!EXACT) {
-        const Refl<T> h = refl_fast(S.x, R);
-        T dot = a[0];
-#pragma unroll
-        for (int r = 1; r < 32; ++r)
-            if (r < R) dot = fma(a[r], S.x[r] * h.alpha, dot);
-        const T td = h.tau * dot;
-        a[0] -= td;
-#pragma unroll
-        for (int r = 1; r < 32; ++r)
-            if (r < R) a[r] = fma(-td, S.x[r] * h.alpha, a[r]);
-    } else {
-#pragma clang fp contract(off)
-        const Refl<T> h = refl_exact(S.x, R);
-        for (int r = lane; r < R; r += 64) S.w[r] = (r == 0) ? (T)1. : S.x[r] * h.alpha;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const T mt = -h.tau;
-        for (int e = lane; e < R * R; e += 64) {
-            const int r = e / R, k = e - r * R;
-            T v = ((T)0 + S.w[r] * S.w[k]) * mt;
-            if (r == k) v = 1 + v;
-            S.H[r * 33 + k] = v;
-        }
-        T *my = S.buf + lane * 33;
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-            if (r < R) my[r] = a[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // A_t <- H A_t : out[r] = sum_k H[r][k] a[k]
-        for (int r = 0; r < R; ++r) {
-            T acc = (T)0;
-            for (int k = 0; k < R; ++k) acc += S.H[r * 33 + k] * my[k];
-#pragma unroll
-            for (int rr = 0; rr < 32; ++rr)
-                if (rr == r) a[rr] = acc;
-        }
-    }
+    for (int r = 0; r < 32; ++r) a[r] = (lane < L && r < R) ? A.ld(A.row(i1 + r) + col) : (T)0;
+    refl_apply<T, EXACT>(a, R, S, lane, false);
     if (lane < L) {
 #pragma unroll
         for (int r = 0; r < 32; ++r)
-            if (r < R) st_c(colp + (long)r * lda, a[r]);
+            if (r < R) A.st(A.row(i1 + r) + col, a[r]);
+    }
+}
+
+// ---- full interior windows in the LDS ring, fast mode, compile-time B ------
+// Away from the matrix edge every right window is 2B x B and every left window
+// B x 2B (B = b).  These paths carry no per-element predicates: every lane
+// reads the reflector source x as an LDS broadcast and forms alpha and tau
+// itself (no serial lane-0 section), and w_c = alpha x_c is folded into the
+// dot product and the update:
+//   sigma = sum_{c>=1} a_c x_c,  dot = a_0 + alpha sigma,  a_0 -= tau dot,
+//   a_c -= (tau dot alpha) x_c.
+template <typename T, int N>
+__device__ __forceinline__ void refl_scalars(const T (&x)[N], T &alpha, T &tau) {
+    T q0 = (T)0, q1 = (T)0, q2 = (T)0, q3 = (T)0;
+#pragma unroll
+    for (int r = 0; r < N; r += 4) {
+        q0 = fma(x[r], x[r], q0);
+        if (r + 1 < N) q1 = fma(x[r + 1], x[r + 1], q1);
+        if (r + 2 < N) q2 = fma(x[r + 2], x[r + 2], q2);
+        if (r + 3 < N) q3 = fma(x[r + 3], x[r + 3], q3);
+    }
+    const T nrm = sqrt((q0 + q1) + (q2 + q3));
+    const double s = x[0] >= (T)0 ? -1.0 : 1.0;
+    const double u1 = (double)x[0] - s * (double)nrm;
+    alpha = (T)(1. / u1);
+    tau = (T)(-s * u1 / (double)nrm);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void refl_update(T (&a)[N], const T (&x)[N], T alpha, T tau) {
+    T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+    for (int c = 1; c < N; c += 4) {
+        s0 = fma(a[c], x[c], s0);
+        if (c + 1 < N) s1 = fma(a[c + 1], x[c + 1], s1);
+        if (c + 2 < N) s2 = fma(a[c + 2], x[c + 2], s2);
+        if (c + 3 < N) s3 = fma(a[c + 3], x[c + 3], s3);
+    }
+    const T dot = fma(alpha, (s0 + s1) + (s2 + s3), a[0]);
+    const T td = tau * dot;
+    a[0] -= td;
+    const T tda = td * alpha;
+#pragma unroll
+    for (int c = 1; c < N; ++c) a[c] = fma(-tda, x[c], a[c]);
+}
+
+// right window rows [i1, i1+2B) x cols [j1, j1+B); lane = row - i1 (lanes >= 2B idle)
+template <typename T, int B>
+__device__ __forceinline__ void win_right_full(const RingAcc<T> &A, int i1, int j1, int lane) {
+    const int r = i1 + (lane < 2 * B ? lane : 0);
+    const T *px = A.row(i1) + j1;
+    T *pa = A.row(r) + j1;
+    T a[B], x[B];
+#pragma unroll
+    for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
+    T alpha, tau;
+    refl_scalars<T, B>(x, alpha, tau);
+    refl_update<T, B>(a, x, alpha, tau);
+    if (lane < 2 * B) {
+#pragma unroll
+        for (int c = 0; c < B; ++c) pa[c] = a[c];
+    }
+}
+
+// left window rows [i1, i1+B) x cols [j1, j1+2B); lane = col - j1 (lanes >= 2B idle)
+template <typename T, int B>
+__device__ __forceinline__ void win_left_full(const RingAcc<T> &A, int i1, int j1, int lane) {
+    const int col = lane < 2 * B ? lane : 0;
+    int slot = A.slot(i1);
+    T a[B], x[B];
+    T *rows[B];
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+        rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
+        x[r] = rows[r][0];
+        a[r] = rows[r][col];
+        slot = slot + 1 == A.R ? 0 : slot + 1;
+    }
+    T alpha, tau;
+    refl_scalars<T, B>(x, alpha, tau);
+    refl_update<T, B>(a, x, alpha, tau);
+    if (lane < 2 * B) {
+#pragma unroll
+        for (int r = 0; r < B; ++r) rows[r][col] = a[r];
     }
 }
 
@@ -257,19 +403,14 @@ struct SweepIter {
         }
         return w;
     }
+    // Top row of task t+1 given the state after task t (window tops are
+    // non-decreasing along a sweep); m once the sweep is finished.
+    __device__ int next_top(int t) const {
+        if (t + 1 >= ntask) return m;
+        return t == 0 ? i + 1 : tl.i1;
+    }
 };
 
-// Pipelined sweeps.  Sweep i runs on wave i mod NW of a persistent grid and
-// executes its tasks in order; task t of sweep i may start once task t+3 of
-// sweep i-1 has finished (or sweep i-1 is complete).  Lag 3 is the smallest
-// lag for which every pair of overlapping windows keeps the reference's
-// serial order (checked exhaustively over the geometry in
-// tests/test_stage2_schedule.py), so the result equals the serial sweep's --
-// bit for bit in exact-order mode.
-// Hand-off (MI355X_MICROARCH.md, valid forms, table row 1): every band access
-// is an sc1 load/store, the producing wave drains its stores
-// (s_waitcnt vmcnt(0)) before its sc1 progress-flag store, and the consuming
-// wave polls that flag with sc1 loads before its own sc1 loads.
 constexpr int kSpinLimit = 1 << 24;
 
 __device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i) {
@@ -278,6 +419,17 @@ __device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i) {
     return it.ntask;
 }
 
+// ==========================================================================
+// k_band2bd_pipe: sweep i runs on wave i mod NW of a persistent grid and
+// executes its tasks in order; task t of sweep i may start once task t+3 of
+// sweep i-1 has finished (or sweep i-1 is complete).  Lag 3 is the smallest
+// lag for which every pair of overlapping windows keeps the reference's
+// serial order (checked exhaustively in tests/test_stage2_schedule.py).
+// Hand-off (MI355X_MICROARCH.md, valid forms, table row 1): every band access
+// is an sc1 load/store, the producing wave drains its stores
+// (s_waitcnt vmcnt(0)) before its sc1 progress-flag store, and the consuming
+// wave polls that flag with sc1 loads before its own sc1 loads.
+// ==========================================================================
 template <typename T, bool EXACT>
 __global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long lda, int b, int *prog,
                                                      int *err)
@@ -285,6 +437,7 @@ __global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long ld
     __shared__ WaveLds<T, EXACT> S;
     const int lane = threadIdx.x;
     const int nw = gridDim.x;
+    const HbmAcc<T> acc{A, lda};
     for (int i = blockIdx.x; i < n - 1; i += nw) {
         SweepIter it;
         it.init(m, n, b, i);
@@ -308,13 +461,373 @@ __global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long ld
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             if (wnd.j2 > wnd.j1 && wnd.i2 > wnd.i1) {
-                if (right) win_right<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
-                else       win_left<T, EXACT>(A, lda, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
+                if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
+                else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, S, lane);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             if (lane == 0) __hip_atomic_store(prog + i, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+}
+
+// ==========================================================================
+// k_band2bd_bundle: workgroup = S compute waves + loader + writer; bundle beta =
+// sweeps beta*S .. beta*S+S-1, bundles dealt round-robin to a persistent grid.
+//
+// LDS ring: band row r (diagonals -(b-1)..2b-1, every element any window can
+// touch) lives in slot r % R while the bundle works on it.  Compute wave s runs
+// sweep beta*S+s on the ring with the lag-3 rule against wave s-1 (LDS
+// progress flags) and publishes the top row of its next window ("front").
+// The loader wave fills the ring ahead of the sweeps, 16 rows per batch, as
+// far as the ring allows (slot r is free once the writer has read row r-R)
+// and as far as bundle beta-1 has finished (its rows_done counter).  The
+// writer wave writes back every row below all fronts (no sweep of the bundle
+// touches it again) and advances rows_done[beta].
+// Bundle beta+1 loads a row only after bundle beta is done with it, so every
+// element still sees the reference's serial order.  Row hand-offs between
+// bundles use the sc1 protocol of k_band2bd_pipe.
+// ==========================================================================
+struct BundleFlags {
+    int prog[16];    // tasks completed per compute wave
+    int front[16];   // top row of each wave's next window (n when done)
+    int loaded;      // rows < loaded are in the ring (loader wave)
+    int freed;       // ring slots of rows < freed may be reused (writer wave)
+};
+
+__device__ __forceinline__ int lds_acq(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_rel(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// fp64 bundles are LDS-limited to S <= 3 compute waves (+ loader + writer),
+// which leaves the compute waves the registers of a 320-thread launch bound;
+// fp32 bundles to about 7, capped at 6 (512 threads, 256 VGPRs per wave).
+template <typename T> constexpr int bundle_max_threads() { return sizeof(T) == 8 ? 320 : 512; }
+constexpr int kBankRows = 16;   // rows per loader register bank (two banks)
+constexpr int kWriteRows = 16;  // rows per writer iteration (at most)
+
+// s_waitcnt vmcnt(k) for a run-time k in [0, 2 kWriteRows] (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int k) {
+    switch (k) {
+#define BRD_VMCNT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        BRD_VMCNT_CASE(1) BRD_VMCNT_CASE(2) BRD_VMCNT_CASE(3) BRD_VMCNT_CASE(4) BRD_VMCNT_CASE(5)
+        BRD_VMCNT_CASE(6) BRD_VMCNT_CASE(7) BRD_VMCNT_CASE(8) BRD_VMCNT_CASE(9) BRD_VMCNT_CASE(10)
+        BRD_VMCNT_CASE(11) BRD_VMCNT_CASE(12) BRD_VMCNT_CASE(13) BRD_VMCNT_CASE(14) BRD_VMCNT_CASE(15)
+        BRD_VMCNT_CASE(16) BRD_VMCNT_CASE(17) BRD_VMCNT_CASE(18) BRD_VMCNT_CASE(19) BRD_VMCNT_CASE(20)
+        BRD_VMCNT_CASE(21) BRD_VMCNT_CASE(22) BRD_VMCNT_CASE(23) BRD_VMCNT_CASE(24) BRD_VMCNT_CASE(25)
+        BRD_VMCNT_CASE(26) BRD_VMCNT_CASE(27) BRD_VMCNT_CASE(28) BRD_VMCNT_CASE(29) BRD_VMCNT_CASE(30)
+        BRD_VMCNT_CASE(31) BRD_VMCNT_CASE(32)
+#undef BRD_VMCNT_CASE
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+template <typename T> constexpr int kEpp = 16 / sizeof(T);   // elements per 16-byte piece
+constexpr int kRsrcWord3 = 0x00020000;                       // raw buffer descriptor word 3 (gfx9 family)
+
+// Ring row pitch: diagonals -(b-1) .. 2b-1 (3b-1 elements), rounded up to a
+// multiple of 16 bytes (rows move as 16-byte pieces: LDS-DMA in, b128 out),
+// which also leaves consecutive rows (a right window's lanes) an odd number
+// of elements apart: conflict-free LDS access.
+template <typename T>
+__host__ __device__ constexpr int ring_pitch(int b) {
+    return (3 * b - 1 + (int)(16 / sizeof(T)) - 1) / (int)(16 / sizeof(T)) * (int)(16 / sizeof(T));
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte agent-coherent (sc1, write-through) store
+__device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <typename T, bool EXACT, int KB>
+__global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R,
+                                                         unsigned magic, int *rows_done, int *err)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int P = ring_pitch<T>(b);
+    T *ring = (T *)smem;
+    const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
+    WaveLds<T, EXACT> *wl = (WaveLds<T, EXACT> *)(smem + ring_bytes);
+    BundleFlags *F = (BundleFlags *)(wl + S);
+    // readfirstlane: the compiler then keeps all window geometry in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const RingAcc<T> acc{ring, P, R, b - 1, magic};
+    const int nbundles = (n - 1 + S - 1) / S;
+
+    for (int beta = blockIdx.x; beta < nbundles; beta += gridDim.x) {
+        const int i0 = beta * S;
+        const int nsw = min(S, n - 1 - i0);
+        if (threadIdx.x < 16) {
+            F->prog[threadIdx.x] = 0;
+            F->front[threadIdx.x] = (int)threadIdx.x < nsw ? i0 + (int)threadIdx.x : n;
+        }
+        if (threadIdx.x == 0) { F->loaded = i0; F->freed = i0; }
+        __syncthreads();
+        if (threadIdx.x == 0) S2STAMP(beta, 0);
+
+        if (wave < nsw) {
+            // ---------------- compute wave: sweep i0 + wave ----------------
+            const int i = i0 + wave;
+            SweepIter it;
+            it.init(n, n, b, i);
+            const int prev_ntask = wave > 0 ? sweep_ntask(n, n, b, i - 1) : 0;
+            for (int t = 0; t < it.ntask; ++t) {
+                bool right;
+                const Win wnd = it.task(t, right);
+                const bool live = wnd.j2 > wnd.j1 && wnd.i2 > wnd.i1;
+                int spins = 0;
+                unsigned long long c0 = S2CLK();
+                if (wave > 0) {
+                    const int need = min(t + 4, prev_ntask);
+                    while (lds_acq(&F->prog[wave - 1]) < need) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
+                    }
+                }
+                unsigned long long c1 = S2CLK();
+                S2ACC(beta, wave * 3, c0, c1);
+                if (live) {
+                    while (lds_acq(&F->loaded) < wnd.i2) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 3); break; }
+                    }
+                    c0 = S2CLK();
+                    S2ACC(beta, wave * 3 + 1, c1, c0);
+                    const int wr = wnd.i2 - wnd.i1, wc = wnd.j2 - wnd.j1;
+                    if constexpr (KB > 0) {
+                        if (right && wr == 2 * KB && wc == KB)
+                            win_right_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
+                        else if (!right && wr == KB && wc == 2 * KB)
+                            win_left_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
+                        else if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                        else            win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                    } else {
+                        if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                        else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                    }
+                    c1 = S2CLK();
+                    S2ACC(beta, wave * 3 + 2, c0, c1);
+                }
+                if (lane == 0) {
+                    lds_rel(&F->front[wave], it.next_top(t));
+                    lds_rel(&F->prog[wave], t + 1);
+                    if (wave == 0 && t == 0) S2STAMP(beta, 1);
+                }
+            }
+            if (lane == 0 && wave == 0) S2STAMP(beta, 2);
+            if (lane == 0 && wave == nsw - 1) S2STAMP(beta, 3);
+        } else if (wave == S) {
+            // ---------------- loader wave: HBM -> registers -> ring ----------------
+            // Two register banks of kBankRows rows each (16-byte pieces, lane q
+            // holds piece q of every row) are fetched ahead with sc1 loads;
+            // when ring slots free up a bank is written with ds_write_b128 and
+            // refetched, so the ring's refill latency is an LDS latency, not an
+            // HBM round trip.  A bank is fetched only once bundle beta-1 has
+            // finished its rows (buffer loads with sc1; the compiler counts
+            // the outstanding loads, so the older bank is retired by a
+            // vmcnt(kBankRows) wait while the younger stays in flight).
+            const int row_q = P * (int)sizeof(T) / 16;
+            const int *done_prev = beta > 0 ? rows_done + beta - 1 : nullptr;
+            int avail = done_prev ? __builtin_amdgcn_readfirstlane(ld_c(done_prev)) : n;
+            int spins = 0;
+            auto need_avail = [&](int hi) {      // wait until bundle beta-1 is done with rows < hi
+                hi = min(hi, n);
+                while (avail < hi) {
+                    __builtin_amdgcn_s_sleep(1);
+                    avail = __builtin_amdgcn_readfirstlane(ld_c(done_prev));
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 4); return false; }
+                }
+                return true;
+            };
+            auto fetch = [&](u32x4 (&bk)[kBankRows], int r0) {
+#pragma unroll
+                for (int rr = 0; rr < kBankRows; ++rr) {
+                    const int r = min(r0 + rr, n - 1);
+                    const int c0 = r - (b - 1) + (lane < row_q ? lane : 0) * kEpp<T>;
+                    // buffer descriptor at the row start (always inside the matrix), sc1
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)(A + (long)r * lda), 0, 0x7fffffff, kRsrcWord3);
+                    // wave-uniform choice per row: exactly one load path runs, so
+                    // no load waits on another's destination registers
+                    if (r >= b - 1 && r - (b - 1) + P <= n) {
+                        bk[rr] = __builtin_amdgcn_raw_buffer_load_b128(rs, c0 * (int)sizeof(T), 0, 16);
+                    } else {
+                        // edge row: element loads at clamped columns (the columns
+                        // outside the matrix are zeroed when the bank is stored)
+                        T e[kEpp<T>];
+#pragma unroll
+                        for (int k = 0; k < kEpp<T>; ++k) {
+                            const int c = min(max(c0 + k, 0), n - 1);
+                            if constexpr (sizeof(T) == 8) {
+                                const auto w = __builtin_amdgcn_raw_buffer_load_b64(rs, c * 8, 0, 16);
+                                __builtin_memcpy(&e[k], &w, 8);
+                            } else {
+                                const auto w = __builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, 16);
+                                __builtin_memcpy(&e[k], &w, 4);
+                            }
+                        }
+                        __builtin_memcpy(&bk[rr], e, 16);
+                    }
+                }
+            };
+            auto store = [&](u32x4 (&bk)[kBankRows], int r0) {
+#pragma unroll
+                for (int rr = 0; rr < kBankRows; ++rr) {
+                    const int r = r0 + rr;
+                    if (r < n && lane < row_q) {
+                        const int c0 = r - (b - 1) + lane * kEpp<T>;
+                        u32x4 v = bk[rr];
+                        if (!(c0 >= 0 && c0 + kEpp<T> <= n)) {     // edge piece: zero outside the matrix
+                            T e[kEpp<T>];
+                            __builtin_memcpy(e, &v, 16);
+#pragma unroll
+                            for (int k = 0; k < kEpp<T>; ++k)
+                                if (c0 + k < 0 || c0 + k >= n) e[k] = (T)0;
+                            __builtin_memcpy(&v, e, 16);
+                        }
+                        *(u32x4 *)(ring + acc.slot(r) * P + lane * kEpp<T>) = v;
+                    }
+                }
+            };
+            auto need_ring = [&](int hi) {       // ring slots for rows < hi are free
+                hi = min(hi, n);
+                while (__builtin_amdgcn_readfirstlane(lds_acq(&F->freed)) + R < hi) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 6); return false; }
+                }
+                return true;
+            };
+            u32x4 bA[kBankRows], bB[kBankRows];
+            int ra = i0, rb = i0 + kBankRows;
+            unsigned long long c0 = S2CLK();
+            bool ok = need_avail(ra + kBankRows);
+            fetch(bA, ra);
+            ok = ok && need_avail(rb + kBankRows);
+            fetch(bB, rb);
+            while (ok && ra < n) {
+                unsigned long long c1 = S2CLK();
+                S2ACC(beta, 9, c0, c1);
+                ok = need_ring(ra + kBankRows);
+                c0 = S2CLK();
+                S2ACC(beta, 10, c1, c0);
+                store(bA, ra);
+                if (lane == 0) lds_rel(&F->loaded, min(ra + kBankRows, n));
+                ra += 2 * kBankRows;
+                c1 = S2CLK();
+                S2ACC(beta, 11, c0, c1);
+                c0 = c1;
+                ok = ok && need_avail(ra + kBankRows);
+                fetch(bA, ra);
+                if (!ok || rb >= n) break;
+                c1 = S2CLK();
+                S2ACC(beta, 9, c0, c1);
+                ok = need_ring(rb + kBankRows);
+                c0 = S2CLK();
+                S2ACC(beta, 10, c1, c0);
+                store(bB, rb);
+                if (lane == 0) lds_rel(&F->loaded, min(rb + kBankRows, n));
+                rb += 2 * kBankRows;
+                c1 = S2CLK();
+                S2ACC(beta, 11, c0, c1);
+                c0 = c1;
+                ok = ok && need_avail(rb + kBankRows);
+                fetch(bB, rb);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) S2STAMP(beta, 5);
+        } else if (wave == S + 1) {
+            // ---------------- writer wave: ring -> HBM ----------------
+            // Writes every row below all fronts (no sweep of the bundle touches
+            // it again), <= kWriteRows per iteration: ring -> registers (the
+            // slots are freed at once) -> 16-byte sc1 stores.  Store completion
+            // is pipelined two iterations deep: after issuing k stores, a
+            // vmcnt(k + k_prev) wait retires the iteration before the previous
+            // one, whose end row is then published in rows_done[beta].
+            const int row_q = P * (int)sizeof(T) / 16;
+            int wb = i0, spins = 0;
+            int pend0 = -1, pend1 = -1, k1 = 0;  // end rows of the two iterations in flight; stores of the younger
+            unsigned long long c0 = S2CLK();
+            while (wb < n) {
+                int fmin = n;
+                for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
+                const int wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_acq(&F->loaded)), wb + kWriteRows));
+                if (wt <= wb) {
+                    if (pend1 >= 0 || pend0 >= 0) {   // nothing new: retire everything in flight
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) st_c(rows_done + beta, pend1 >= 0 ? pend1 : pend0);
+                        pend0 = pend1 = -1;
+                        k1 = 0;
+                    }
+                    const unsigned long long c1 = S2CLK();
+                    S2ACC(beta, 12, c0, c1);
+                    c0 = c1;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 5); break; }
+                    continue;
+                }
+                spins = 0;
+                const int k = wt - wb;
+                u32x4 v[kWriteRows];
+#pragma unroll
+                for (int rr = 0; rr < kWriteRows; ++rr) {
+                    const int r = min(wb + rr, wt - 1);
+                    const u32x4 *src = (const u32x4 *)(ring + acc.slot(r) * P);
+                    v[rr] = src[lane < row_q ? lane : 0];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) lds_rel(&F->freed, wt);   // slots reusable once read
+                const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
+                if (interior) {
+#pragma unroll
+                    for (int rr = 0; rr < kWriteRows; ++rr) {
+                        if (rr < k) {
+                            const int r = wb + rr;
+                            T *g = A + (long)r * lda + r - (b - 1);
+                            if (lane < row_q) st16_sc1((char *)g + 16 * lane, v[rr]);
+                        }
+                    }
+                    // retire everything but this iteration's and the previous one's stores
+                    wait_vmcnt(k + k1);
+                    if (pend0 >= 0 && lane == 0) st_c(rows_done + beta, pend0);
+                    pend0 = pend1;
+                    pend1 = wt;
+                    k1 = k;
+                } else {
+#pragma unroll
+                    for (int rr = 0; rr < kWriteRows; ++rr) {
+                        const int r = wb + rr;
+                        if (r < wt && lane < row_q) {
+                            T *g = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
+                            const int c0 = r - (b - 1) + lane * kEpp<T>;
+                            T e[kEpp<T>];
+                            __builtin_memcpy(e, &v[rr], 16);
+#pragma unroll
+                            for (int kk = 0; kk < kEpp<T>; ++kk)
+                                if (c0 + kk >= 0 && c0 + kk < n) st_c(g + kk, e[kk]);
+                        }
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) st_c(rows_done + beta, wt);
+                    pend0 = pend1 = -1;
+                    k1 = 0;
+                }
+                wb = wt;
+                {
+                    const unsigned long long c1 = S2CLK();
+                    S2ACC(beta, 13, c0, c1);
+                    c0 = c1;
+                }
+            }
+            if (pend1 >= 0 || pend0 >= 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) st_c(rows_done + beta, pend1 >= 0 ? pend1 : pend0);
+            }
+            if (lane == 0) S2STAMP(beta, 4);
+        }
+        __syncthreads();
     }
 }
 
@@ -326,7 +839,39 @@ __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
     if (i < n - 1) e[i] = A[(long)i * lda + i + 1];
 }
 
-// prog: n ints, err: 1 int (device workspace, zeroed here).
+// ---- bundle geometry ---------------------------------------------------------
+// Ring rows needed for S sweeps to make progress: the leading sweep may have to
+// run 3(S-1) tasks (1.5(S-1) window pairs of b rows) ahead of the trailing one,
+// plus a 2b-row window, plus S rows of sweep shift; checked against the exact
+// geometry in tests/test_stage2_schedule.py.
+int ring_min_rows(int b, int S) { return ((3 * (S - 1) + 1) / 2) * b + 2 * b + S + 8; }
+
+template <typename T, bool EXACT>
+static size_t bundle_lds_bytes(int b, int S, int R) {
+    const size_t ring = ((size_t)R * ring_pitch<T>(b) * sizeof(T) + 15) & ~(size_t)15;
+    return ring + (size_t)S * sizeof(WaveLds<T, EXACT>) + sizeof(BundleFlags);
+}
+
+template <typename T, bool EXACT>
+static bool bundle_plan(int n, int b, int &S, int &R) {
+    const size_t budget = 160 * 1024 - 512;
+    static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
+    int smax = EXACT ? 2 : bundle_max_threads<T>() / 64 - 2;
+    if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
+    for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
+        // + one loader bank: the loader hands rows over kBankRows at a time
+        const int rmin = ring_min_rows(b, S) + kBankRows;
+        if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
+            // largest ring that fits (more prefetch slack), but no more than n rows
+            R = rmin;
+            while (R < n + 1 && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
+            return true;
+        }
+    }
+    return false;
+}
+
+// prog: n+1 ints, err: 1 int (device workspace, zeroed here).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *prog, int *err,
                           int nwaves, hipStream_t s)
@@ -335,6 +880,29 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *p
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
+    static const char *sel = getenv("BRD_S2_SCHEDULE");   // "pipe" selects the HBM-only schedule
+    const bool pipe = sel && sel[0] == 'p';
+    int S = 0, R = 0;
+    const bool ok = exact_order ? bundle_plan<T, true>(n, b, S, R) : bundle_plan<T, false>(n, b, S, R);
+    if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule (the loader assumes n >= 16 / sizeof(T))
+        const int nbundles = (n - 1 + S - 1) / S;
+        const int grid = std::max(1, std::min(nwaves, nbundles));
+        const dim3 block(64 * (S + 2));
+        const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
+        const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0>
+                         : b == 32   ? (const void *)k_band2bd_bundle<T, false, 32>
+                                     : (const void *)k_band2bd_bundle<T, false, 0>;
+        const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        if (exact_order)
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+        else if (b == 32)
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+        else
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+        return hipGetLastError();
+    }
     const int grid = std::max(1, std::min(nwaves, n - 1));
     if (exact_order)
         hipLaunchKernelGGL((k_band2bd_pipe<T, true>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, prog, err);

@@ -69,3 +69,31 @@ def test_windows_fit_kernel_limits():
                     assert rows <= max(2 * b, b + 1) and cols <= b
                 else:
                     assert rows <= b and cols <= 2 * b
+
+
+def ring_min_rows(b, S):
+    """Mirror of brd_stage2.hip ring_min_rows()."""
+    return ((3 * (S - 1) + 1) // 2) * b + 2 * b + S + 8
+
+
+def exact_ring_need(n, b, S):
+    """Rows the LDS ring must hold so the trailing sweep of a bundle can always
+    progress: from the trailing sweep's next window top to the bottom of the
+    leading sweep's window 3(S-1) tasks ahead (its predecessors' bottoms are
+    at most S-1 rows lower)."""
+    W = windows(n, n, b)
+    worst = 0
+    for i0 in range(0, n - S):
+        lead, trail = W[i0], W[i0 + S - 1]
+        for tau, w in enumerate(trail):
+            if w is None:
+                continue
+            hi = min(tau + 3 * (S - 1), len(lead) - 1)
+            bots = [x[1] for x in lead[:hi + 1] if x is not None] + [w[1]]
+            worst = max(worst, max(bots) + (S - 1) - w[0])
+    return worst
+
+
+@pytest.mark.parametrize("n,b,S", [(300, 32, 1), (300, 32, 2), (300, 32, 3), (300, 32, 7), (200, 4, 15), (120, 8, 5)])
+def test_ring_size_formula_is_sufficient(n, b, S):
+    assert ring_min_rows(b, S) >= exact_ring_need(n, b, S)

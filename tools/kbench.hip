@@ -4,10 +4,15 @@
 //         -Lsvdsolver_amd/lib -lbrd_hip -Wl,-rpath,$PWD/svdsolver_amd/lib -o /tmp/kbench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "brd_internal.h"
 namespace brd { hipError_t read_stamps(unsigned long long *out); }
 using namespace brd;
+static void check_err(const char *what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e)); exit(3); }
+}
 int main(int argc, char **argv) {
     int n = argc > 1 ? atoi(argv[1]) : 8192;
     int b = 32;
@@ -26,6 +31,7 @@ int main(int argc, char **argv) {
             launch_factor<double>(trans, A, n, t, lvl, w, 0);
             hipEventRecord(e1); hipEventSynchronize(e1);
             float ms; hipEventElapsedTime(&ms, e0, e1);
+            check_err("factor");
             unsigned long long st[64]; read_stamps(st);
             printf("factor trans=%d level=%d groups=%d: %.1f us | stamps(cyc):", trans, lvl, t.lv[lvl].groups, ms * 1e3);
             for (int k = 1; k <= 6; ++k) printf(" %llu", st[k] - st[k - 1]);
@@ -38,6 +44,7 @@ int main(int argc, char **argv) {
             launch_apply<double>(trans, A, n, t, 0, n - b, w, 0);
             hipEventRecord(e1); hipEventSynchronize(e1);
             float ms; hipEventElapsedTime(&ms, e0, e1);
+            check_err("apply");
             double fl = 4.0 * b * n * (double)(n - b);
             printf("apply trans=%d level0 M=%d ncols=%d: %.1f us  %.1f TF/s  %.0f GB/s\n", trans, n, n - b, ms * 1e3,
                    fl / (ms * 1e-3) / 1e12, 16.0 * n * (double)(n - b) / (ms * 1e-3) / 1e9);

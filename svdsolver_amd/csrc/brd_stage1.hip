@@ -26,6 +26,7 @@
 #include "brd_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace brd {
 
@@ -40,8 +41,24 @@ __device__ unsigned long long g_stamps[64];
 hipError_t read_stamps(unsigned long long *out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
 }
+// per-phase cycle accumulators of the k_factor column loop (wave 0 of workgroup 0)
+#define PH_DECL unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph_acc[5] = {0, 0, 0, 0, 0}
+#define PH(k)                                                                      \
+    do {                                                                           \
+        const unsigned long long ph_n = __builtin_amdgcn_s_memtime();              \
+        ph_acc[k] += ph_n - ph_t;                                                  \
+        ph_t = ph_n;                                                               \
+    } while (0)
+#define PH_STORE                                                                   \
+    do {                                                                           \
+        if (blockIdx.x == 0 && threadIdx.x == 0)                                   \
+            for (int k = 0; k < 5; ++k) g_stamps[10 + k] = ph_acc[k];              \
+    } while (0)
 #else
 #define STAMP(k) do {} while (0)
+#define PH_DECL do {} while (0)
+#define PH(k) do {} while (0)
+#define PH_STORE do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------
@@ -105,28 +122,132 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // ==========================================================================
-// k_factor: Householder QR of one tree node.
-// 512 threads = 16 row groups (rg) x 32 columns (c); thread (rg,c) keeps
-// rows rg, rg+16, ... of column c in registers (rows >= nr are zero).  Per
-// column j one workgroup reduction yields G_c = sum_{i>j} X[i][j] X[i][c] for
-// every c, from which the reflector, the projections w_c = v_j^T X[:,c]
-// (c > j) and the inner products v_c^T v_j (c < j, for T) all follow.
-// Columns are kept unscaled ("raw") while the panel is factored:
-// v_j = X[:,j] / u1_j below the diagonal.
+// Cross-lane helpers (gfx950).  wave_sum: butterfly over the 64 lanes --
+// DPP xor-1 / xor-2 (quad_perm), mirror-8, mirror-16, then v_permlane16_swap
+// (row pairs) and v_permlane32_swap (halves); every lane gets the total.
 // ==========================================================================
-constexpr int kFT = 512;         // threads per factor workgroup
-constexpr int kRG = kFT / 32;    // row groups
-constexpr int kQ = kRmax / kRG;  // rows per thread
-constexpr int kFS = 33;          // LDS row stride of the staging tile
+#define BRD_DPP32(x, ctrl) __builtin_amdgcn_update_dpp(0, (x), (ctrl), 0xf, 0xf, false)
 
-// Row j < 32 of the tile lives in register slot j / kRG, i.e. slot 0 or 1:
-// two-way selects keep every register index static (no scratch).
-static_assert(kRG >= 16, "row j < 32 must live in register slot 0 or 1");
-template <typename T, int N>
-__device__ __forceinline__ T slot01_get(const T (&x)[N], int q) { return q == 0 ? x[0] : x[1]; }
-template <typename T, int N>
-__device__ __forceinline__ void slot01_set(T (&x)[N], int q, T v) {
-    if (q == 0) x[0] = v; else x[1] = v;
+__device__ __forceinline__ double dpp64(double x, int) = delete;
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    return __hiloint2double(BRD_DPP32(__double2hiint(x), CTRL), BRD_DPP32(__double2loint(x), CTRL));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __int_as_float(BRD_DPP32(__float_as_int(x), CTRL));
+}
+__device__ __forceinline__ double swap_add16(double v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double swap_add32(double v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ float swap_add16(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(a[0]) + __int_as_float(a[1]);
+}
+__device__ __forceinline__ float swap_add32(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(a[0]) + __int_as_float(a[1]);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);   // row_half_mirror
+    v += dpp<0x140>(v);   // row_mirror
+    v = swap_add16(v);
+    return swap_add32(v);
+}
+// permlane swaps on whole values: {a', b'} per v_permlane{16,32}_swap_b32
+// (16: odd rows of a <-> even rows of b; 32: upper half of a <-> lower half of b)
+__device__ __forceinline__ void swap16(double &a, double &b) {
+    const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    a = __hiloint2double(h[0], l[0]);
+    b = __hiloint2double(h[1], l[1]);
+}
+__device__ __forceinline__ void swap32(double &a, double &b) {
+    const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    a = __hiloint2double(h[0], l[0]);
+    b = __hiloint2double(h[1], l[1]);
+}
+__device__ __forceinline__ void swap16(float &a, float &b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false);
+    a = __int_as_float(r[0]);
+    b = __int_as_float(r[1]);
+}
+__device__ __forceinline__ void swap32(float &a, float &b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(b), false, false);
+    a = __int_as_float(r[0]);
+    b = __int_as_float(r[1]);
+}
+// Four wave sums at once (transpose-reduce): a 32-swap folds columns {0,2}
+// and {1,3} into one register each (low / high half), a 16-swap leaves
+// column c in row c (lanes 16c .. 16c+15), four in-row DPP steps finish.
+// Returns the lane's row total; column c's sum is in lane 16c.
+template <typename T>
+__device__ __forceinline__ T wave_sum4(T v0, T v1, T v2, T v3) {
+    swap32(v0, v2);
+    swap32(v1, v3);
+    T s02 = v0 + v2, s13 = v1 + v3;   // lanes < 32: col 0 / 1; lanes >= 32: col 2 / 3
+    swap16(s02, s13);
+    T t = s02 + s13;                  // row r: column r
+    t += dpp<0xB1>(t);
+    t += dpp<0x4E>(t);
+    t += dpp<0x141>(t);
+    t += dpp<0x140>(t);
+    return t;
+}
+__device__ __forceinline__ double readlane(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float readlane(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// ==========================================================================
+// k_factor: Householder QR of one tree node (<= kRmax rows x bk <= 32 cols).
+// 512 threads = 8 waves; wave w owns columns 4w .. 4w+3 of the whole node,
+// lane l rows l + 64k (k = 0..7), in registers.  Per column j:
+//   * the owner of column j has published v_j's raw sub-diagonal part and
+//     (1/u1, tau, alpha) in LDS;
+//   * every wave forms w_c = v_j^T X[:,c] for its four columns with in-wave
+//     butterfly sums (no cross-wave reduction), updates X[:,c] -= tau w_c v_j
+//     for c > j, and records v_c^T v_j = w_c / u1_c for c < j (the T factor);
+//   * the owner of column j+1 forms its reflector (norm by a butterfly sum)
+//     and publishes it; one barrier.
+// Columns stay unscaled ("raw") while the panel is factored: v_j =
+// X[:,j] / u1_j below the diagonal.  The j loop is unrolled by 4 so that the
+// owner's column index is static (no register-array indexing).
+// ==========================================================================
+constexpr int kFT = 512;          // threads per factor workgroup
+constexpr int kFR = kRmax / 64;   // rows per lane
+
+template <typename T>
+struct Reflector {
+    T inv_u1, tau, alpha;
+};
+// LAPACK-style (tau = 0 when the sub-column is zero) from the squared norm
+// of the sub-column and the diagonal entry x0.
+template <typename T>
+__device__ __forceinline__ Reflector<T> make_reflector(T sub2, T x0) {
+    Reflector<T> h{(T)1, (T)0, x0};
+    if (sub2 != (T)0) {
+        const T nrm = sqrt(fma(x0, x0, sub2));
+        h.alpha = x0 >= (T)0 ? -nrm : nrm;
+        const T u1 = x0 - h.alpha;
+        h.tau = -u1 / h.alpha;
+        h.inv_u1 = (T)1 / u1;
+    }
+    return h;
 }
 
 template <typename T, bool TR>
@@ -134,18 +255,18 @@ __global__ void __launch_bounds__(kFT)
 k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__restrict__ VTws,
          T *__restrict__ Tws)
 {
-    __shared__ T sX[kRmax * kFS];   // staging tile; during the column loop it
-                                     // holds the broadcast column buffers instead
-    __shared__ T sRed[2][kFT / 64][32];
-    __shared__ T sRow[2][32];
-    __shared__ T sZ[32][33];
+    __shared__ T sV[2][kRmax];        // published reflector column (raw, rows > j), double-buffered
+    __shared__ T sH[2][4];            // its 1/u1, tau, alpha
+    __shared__ T sZ[32][33];          // v_c^T v_j (c < j)
     __shared__ T sT[32][33];
-    __shared__ T sU1[32], sTau[32];
+    __shared__ T sU1[32], sTau[32];   // 1/u1 and tau per column
     __shared__ int sMap[kRmax];
+    __shared__ T sStage[kRmax / 2][33];   // row-major <-> register-layout staging, half a node at a time
 
     const int grp = blockIdx.x;
     const int tid = threadIdx.x;
-    const int c = tid & 31, rg = tid >> 5, lane = tid & 63, w = tid >> 6;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nr = group_nrows(grp, la);
     const int bk = la.bk;
     const int kk = min(nr, bk);
@@ -156,108 +277,114 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
         (&sZ[0][0])[e] = (T)0;
         (&sT[0][0])[e] = (T)0;
     }
-    if (tid < 32) { sU1[tid] = (T)1; sTau[tid] = (T)0; }   // sU1: 1/u1 per column
+    if (tid < 32) { sU1[tid] = (T)1; sTau[tid] = (T)0; }
     __syncthreads();
 
-    // ---- stage the tile into registers ------------------------------------
+    // ---- the tile into registers: x[k][cc] = X[lane + 64k][4w + cc] ----------
     STAMP(1);
-    T xr[kQ];
-    if (!TR) {
-        T tmp[kQ];
+    T x[kFR][4];
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            const int i = rg + kRG * q;
-            const bool ok = i < nr && c < bk;
-            const int pr = ok ? sMap[i] : 0;
-            tmp[q] = ok ? *vptr<false>(base, ld, pr, c) : (T)0;
+    for (int k = 0; k < kFR; ++k) {
+        const int i = lane + 64 * k;
+        const int pr = i < nr ? sMap[i] : 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = 4 * w + cc;
+            x[k][cc] = (i < nr && c < bk) ? *vptr<TR>(base, ld, pr, c) : (T)0;
         }
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) xr[q] = tmp[q];
-    } else {
-        // coalesced: consecutive threads read consecutive logical rows (= physical columns)
-        const int r = tid % kRmax;
-        const bool rok = r < nr;
-        const int pr = rok ? sMap[r] : 0;
-#pragma unroll
-        for (int h = tid / kRmax; h < 2; h += kFT / kRmax) {
-            T tmp[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int cc = h * 16 + k;
-                tmp[k] = (rok && cc < bk) ? *vptr<true>(base, ld, pr, cc) : (T)0;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) sX[r * kFS + h * 16 + k] = tmp[k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) xr[q] = sX[(rg + kRG * q) * kFS + c];
-        __syncthreads();   // sX is reused for the column buffers below
     }
-
     STAMP(2);
-    T colj[kQ];
-    for (int j = 0; j < kk; ++j) {
-        const int pb = j & 1;
-        const int jq = j / kRG, jr = j % kRG;      // row j = (rg jr, slot jq)
-        T *sColj = sX + pb * kRmax;   // column j below the diagonal, zero elsewhere
-        if (j == 1) STAMP(3);
-        // (0) the owner of column j publishes its sub-diagonal part to its own wave
-        if (c == j) {
+
+    // publish column j (owner wave, static local column CC)
+    auto publish = [&](int j, auto cc_tag) {
+        constexpr int CC = decltype(cc_tag)::value;
+        T p = (T)0;
 #pragma unroll
-            for (int q = 0; q < kQ; ++q) sColj[rg + kRG * q] = (rg + kRG * q > j) ? xr[q] : (T)0;
+        for (int k = 0; k < kFR; ++k) {
+            const T v = (lane + 64 * k > j) ? x[k][CC] : (T)0;
+            p = fma(v, v, p);
+            sV[j & 1][lane + 64 * k] = v;
         }
-        wave_sync();
-        // (1) partial G_c = sum_{i>j} X[i][j] X[i][c] over this thread's rows
-        //     (four independent chains)
-        T p4[4] = {(T)0, (T)0, (T)0, (T)0};
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            colj[q] = sColj[rg + kRG * q];
-            p4[q & 3] = fma(colj[q], xr[q], p4[q & 3]);
+        const T sub2 = wave_sum(p);
+        const T x0 = readlane(x[0][CC], j);   // row j lives in lane j, k = 0 (j < 32)
+        const Reflector<T> h = make_reflector(sub2, x0);
+        if (lane == 0) {
+            sH[j & 1][0] = h.inv_u1;
+            sH[j & 1][1] = h.tau;
+            sH[j & 1][2] = h.alpha;
+            sU1[j] = h.inv_u1;
+            sTau[j] = h.tau;
         }
-        T p = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-        p += __shfl_xor(p, 32);
-        if ((lane >> 5) == 0) sRed[pb][w][c] = p;
-        if (rg == jr) sRow[pb][c] = slot01_get(xr, jq);
-        __syncthreads();
-        // (2) reflector (LAPACK-style: tau = 0 when the sub-column is zero)
-        T Gc, Gj;
-        {
-            T gc[kFT / 64], gj[kFT / 64];
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    if (kk > 0 && w == 0) publish(0, I0{});
+    __syncthreads();
+
+    PH_DECL;
+    for (int m = 0; m < 8; ++m) {
+        if (4 * m >= kk) break;
 #pragma unroll
-            for (int ww = 0; ww < kFT / 64; ++ww) { gc[ww] = sRed[pb][ww][c]; gj[ww] = sRed[pb][ww][j]; }
+        for (int t = 0; t < 4; ++t) {
+            const int j = 4 * m + t;
+            if (j >= kk) break;
+            if (j == 1) STAMP(3);
+            const int pb = j & 1;
+            // (1) the reflector column and its scalars
+            T vcol[kFR];
 #pragma unroll
-            for (int h = kFT / 128; h >= 1; h >>= 1)
+            for (int k = 0; k < kFR; ++k) vcol[k] = sV[pb][lane + 64 * k];
+            const T inv_u1 = sH[pb][0], tau = sH[pb][1], alpha = sH[pb][2];
+            PH(0);
+            // (2) w_c = X[j][c] + (sum_{i>j} x_ij x_ic) / u1 for the wave's four columns
+            T wcol[4];
 #pragma unroll
-                for (int ww = 0; ww < h; ++ww) { gc[ww] += gc[ww + h]; gj[ww] += gj[ww + h]; }
-            Gc = gc[0];
-            Gj = gj[0];
-        }
-        const T x0 = sRow[pb][j];
-        T alpha = x0, u1 = (T)1, tau = (T)0;
-        if (Gj != (T)0) {
-            const T nrm = sqrt(fma(x0, x0, Gj));
-            alpha = x0 >= (T)0 ? -nrm : nrm;
-            u1 = x0 - alpha;
-            tau = -u1 / alpha;
-        }
-        const T inv_u1 = (T)1 / u1;
-        const T wc = fma(Gc, inv_u1, sRow[pb][c]);      // v_j^T X[:,c]  (c != j)
-        // (3) rank-1 update of the columns right of j: X[i][c] -= tau w_c v_i
-        if (c > j && c < bk) {
-            const T tw = tau * wc, twu = tw * inv_u1;
+            for (int cc = 0; cc < 4; ++cc) {
+                T p0 = (T)0, p1 = (T)0;
 #pragma unroll
-            for (int q = 0; q < kQ; ++q) xr[q] = fma(-twu, colj[q], xr[q]);   // rows i > j
-            if (rg == jr) slot01_set(xr, jq, slot01_get(xr, jq) - tw);         // row j (v_j = 1)
-        } else if (c == j) {
-            if (rg == jr) slot01_set(xr, jq, alpha);
-            if (rg == 0) { sU1[j] = inv_u1; sTau[j] = tau; }
-        } else if (c < j && rg == 0) {
-            sZ[c][j] = wc * sU1[c];                      // v_c^T v_j  (sU1 holds 1/u1)
+                for (int k = 0; k < kFR; k += 2) {
+                    p0 = fma(vcol[k], x[k][cc], p0);
+                    p1 = fma(vcol[k + 1], x[k + 1][cc], p1);
+                }
+                wcol[cc] = p0 + p1;
+            }
+            {
+                const T tsum = wave_sum4(wcol[0], wcol[1], wcol[2], wcol[3]);
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) wcol[cc] = fma(readlane(tsum, 16 * cc), inv_u1, readlane(x[0][cc], j));
+            }
+            PH(1);
+            // (3) update the columns right of j; v^T v for the columns left of j
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int c = 4 * w + cc;
+                if (c > j && c < bk) {
+                    const T tw = tau * wcol[cc], twu = tw * inv_u1;
+#pragma unroll
+                    for (int k = 0; k < kFR; ++k) x[k][cc] = fma(-twu, vcol[k], x[k][cc]);   // rows > j
+                    if (lane == j) x[0][cc] -= tw;                                          // row j (v_j = 1)
+                } else if (c == j) {
+                    if (lane == j) x[0][cc] = alpha;
+                } else if (c < j) {
+                    if (lane == 0) sZ[c][j] = wcol[cc] * sU1[c];
+                }
+            }
+            PH(2);
+            // (4) the owner of column j+1 publishes its reflector
+            if (j + 1 < kk && w == ((j + 1) >> 2)) {
+                if (t == 0) publish(j + 1, I1{});
+                else if (t == 1) publish(j + 1, I2{});
+                else if (t == 2) publish(j + 1, I3{});
+                else publish(j + 1, I0{});
+            }
+            PH(3);
+            __syncthreads();
+            PH(4);
         }
     }
-    __syncthreads();
+    PH_STORE;
     STAMP(4);
 
     // ---- T (LAPACK larft): T[:, j] = -tau_j T[:, :j] (V^T v_j)[:j], T[j][j] = tau_j
@@ -269,9 +396,10 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
         T trow[32];
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            T s = (T)0;
+            T s4[4] = {(T)0, (T)0, (T)0, (T)0};
 #pragma unroll
-            for (int cc = 0; cc < j; ++cc) s = fma(trow[cc], sZ[cc][j], s);
+            for (int cc = 0; cc < j; ++cc) s4[cc & 3] = fma(trow[cc], sZ[cc][j], s4[cc & 3]);
+            const T s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
             const T tj = j < kk ? sTau[j] : (T)0;
             trow[j] = a < j ? -tj * s : (a == j ? tj : (T)0);
         }
@@ -280,56 +408,65 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
     }
     STAMP(5);
     // ---- outputs ------------------------------------------------------------
+    // V (kRmax x 32 row-major) and VT (32 x kRmax, coalesced) from registers;
+    // R / zeros back into the matrix: coalesced from registers for TR = true,
+    // through the staging tile (256-byte rows) for TR = false.
     T *V = Vws + (size_t)grp * kRmax * 32;
     T *VT = VTws + (size_t)grp * 32 * kRmax;
     const int nrp = (nr + 15) & ~15;
-    const T iu = sU1[c];
-    // V (kRmax x 32, row-major, rows < nrp) from registers; scaled copy to LDS for VT
+    T iu[4];
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-        const int i = rg + kRG * q;
-        T v = (T)0;
-        if (c < kk && i < nr) v = i < c ? (T)0 : (i == c ? (T)1 : xr[q] * iu);
-        if (i < nrp) V[(size_t)i * 32 + c] = v;
-        sX[i * kFS + c] = v;
-    }
-    // R (upper) and zeros back into the matrix (TR=false straight from registers)
-    if (!TR) {
+    for (int cc = 0; cc < 4; ++cc) iu[cc] = sU1[4 * w + cc];
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            const int i = rg + kRG * q;
-            if (i < nr && c < bk) *vptr<false>(base, ld, sMap[i], c) = (c >= i) ? xr[q] : (T)0;
+    for (int k = 0; k < kFR; ++k) {
+        const int i = lane + 64 * k;
+        T v[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = 4 * w + cc;
+            v[cc] = (T)0;
+            if (c < kk && i < nr) v[cc] = i < c ? (T)0 : (i == c ? (T)1 : x[k][cc] * iu[cc]);
         }
-    }
-    __syncthreads();
-    for (int e = tid; e < 32 * 32; e += kFT) Tm[e] = sT[e >> 5][e & 31];
-    // VT (32 x kRmax) -- consecutive threads -> consecutive rows, coalesced
-    {
-        const int i = tid % kRmax;
         if (i < nrp) {
-            for (int h = tid / kRmax; h < 2; h += kFT / kRmax) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) VT[(size_t)(16 * h + k) * kRmax + i] = sX[i * kFS + 16 * h + k];
+            for (int cc = 0; cc < 4; ++cc) {
+                V[(size_t)i * 32 + 4 * w + cc] = v[cc];
+                VT[(size_t)(4 * w + cc) * kRmax + i] = v[cc];   // lanes -> consecutive i
             }
         }
-    }
-    if (TR) {
-        __syncthreads();
+        if constexpr (TR) {
+            if (i < nr) {
+                const int pr = sMap[i];
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) sX[(rg + kRG * q) * kFS + c] = xr[q];
-        __syncthreads();
-        const int i = tid % kRmax;
-        if (i < nr) {
-            const int pr = sMap[i];
-            for (int h = tid / kRmax; h < 2; h += kFT / kRmax) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int cc = 16 * h + k;
-                    if (cc < bk) *vptr<true>(base, ld, pr, cc) = (cc >= i) ? sX[i * kFS + cc] : (T)0;
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int c = 4 * w + cc;
+                    if (c < bk) *vptr<TR>(base, ld, pr, c) = (c >= i) ? x[k][cc] : (T)0;
                 }
             }
         }
     }
+    if constexpr (!TR) {
+        const int c = tid & 31;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int k = 0; k < kFR / 2; ++k)
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int i = lane + 64 * (k + kFR / 2 * h), cg = 4 * w + cc;
+                    sStage[lane + 64 * k][cg] = (cg >= i) ? x[k + kFR / 2 * h][cc] : (T)0;
+                }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kRmax / 2 / 16; ++e) {
+                const int r = (tid >> 5) + 16 * e, i = kRmax / 2 * h + r;
+                if (i < nr && c < bk) *vptr<false>(base, ld, sMap[i], c) = sStage[r][c];
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * 32; e += kFT) Tm[e] = sT[e >> 5][e & 31];
     STAMP(6);
 }
 

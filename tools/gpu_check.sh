@@ -10,5 +10,5 @@ rc=$?; echo "PYTEST rc=$rc"; grep -E "passed|failed|Error" gpurun_out/t_$tag.log
 timeout -k 10 300 python bench.py --n $n --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/b_$tag.log 2>&1 || { echo BENCH FAILED; tail -5 gpurun_out/b_$tag.log; exit 1; }
 grep metric gpurun_out/b_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('value',d['value'],'ms',d['ms_per_step'],'stage',d['stage_ms'],'k',d['kernel_ms_per_step'],'roof',d['roofline']['achieved'])"
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_$tag -o run -- python3 bench.py --n $n --steps 1 --warmup 1 --cpu-baseline off > gpurun_out/p_$tag.log 2>&1 || { echo PROF FAILED; exit 1; }
-python3 tools/kstats.py gpurun_out/prof_$tag/run_results.db | head -12
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 bench.py --n $n --steps 1 --warmup 1 --cpu-baseline off > gpurun_out/p_$tag.log 2>&1 || { echo PROF FAILED; exit 1; }
+f=$(find gpurun_out/prof_$tag -name "*kernel_stats.csv" | head -1); echo "stats: $f"; cut -c1-160 "$f" | head -12

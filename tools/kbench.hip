@@ -35,6 +35,8 @@ int main(int argc, char **argv) {
             unsigned long long st[64]; read_stamps(st);
             printf("factor trans=%d level=%d groups=%d: %.1f us | stamps(cyc):", trans, lvl, t.lv[lvl].groups, ms * 1e3);
             for (int k = 1; k <= 6; ++k) printf(" %llu", st[k] - st[k - 1]);
+            printf(" | loop phases pub/dot/bar/refl/upd:");
+            for (int k = 10; k < 15; ++k) printf(" %llu", st[k]);
             printf("\n");
         }
     }

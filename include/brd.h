@@ -20,8 +20,8 @@
  *                   (svd_parallel.h:640; twin gpu::brd_p2, svd_cpu.h:631) --
  *                   band -> bidiagonal, in place, returning d and e like the
  *                   reference's Bidiagonal{d, e} (svd_parallel.h:691).
- *   brd_dist_*      new (the reference has no multi-GPU path):
- *                   RCCL communicator for the block-column-sharded stage 1.
+ *   brd_dist_*,     new (the reference has no multi-GPU path):
+ *   brd_ge2band_dist_*  block-cyclic column-sharded stage 1 over RCCL / xGMI.
  */
 #ifndef BRD_H_
 #define BRD_H_
@@ -50,8 +50,7 @@ enum brd_status {
 
 /* Stage 1: dense m x n (m >= n) -> upper band, bandwidth b (1 <= b <= 32).
  * On return A holds the band matrix: entries (i,j) with 0 <= j-i <= b, and
- * exact zeros elsewhere.  ngpus must be 1, or equal to the world size given
- * to brd_dist_init (then A is this rank's column shard, see brd_dist_*). */
+ * exact zeros elsewhere.  ngpus must be 1 (multi-GPU: brd_ge2band_dist_*). */
 int brd_ge2band_f64(double *A, int m, int n, int lda, int b, int ngpus, unsigned flags);
 int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned flags);
 
@@ -77,10 +76,39 @@ int brd_profile_reset(void);
 int brd_profile_query(const char *kernel, long long *launches, double *total_ms,
                       double *flops, double *bytes);
 
-/* Multi-GPU (one process per GPU, RCCL over xGMI). */
+/* ---- Multi-GPU stage 1 (one process per GPU) ------------------------------
+ * Layout: 1-D block-cyclic over column panels of width b -- global panel p
+ * (columns [p b, p b + b)) lives on rank p mod P as local panel p / P.  A
+ * rank's shard is m x n_loc (n_loc = brd_dist_local_cols), row-major with
+ * leading dimension lda_loc, in device memory.  The stage-2 input is
+ * assembled on one rank with brd_dist_gather_band.
+ * Collectives go to RCCL over xGMI (brd_dist_init, with an id from
+ * brd_dist_unique_id on one rank, shared out of band) or to a host callback
+ * (brd_dist_init_host: the library drains its stream, then calls fn, which
+ * must complete the collective on the device buffers before returning). */
+enum brd_coll_op {
+    BRD_COLL_BCAST = 0,         /* recv (== send) broadcast from root, count elems */
+    BRD_COLL_ALLGATHER = 1,     /* send: count elems; recv: count * nranks elems    */
+    BRD_COLL_ALLREDUCE_SUM = 2  /* in place (send == recv), count elems             */
+};
+enum brd_dtype { BRD_DT_BYTE = 0, BRD_DT_F32 = 1, BRD_DT_F64 = 2 };
+typedef int (*brd_coll_fn)(int op, const void *send, void *recv, unsigned long count, int dtype, int root,
+                           void *user);
+
 int brd_dist_unique_id(void *id_out, int id_bytes);      /* id_bytes >= 128 */
 int brd_dist_init(int rank, int nranks, const void *id, int id_bytes);
+int brd_dist_init_host(int rank, int nranks, brd_coll_fn fn, void *user);
 int brd_dist_finalize(void);
+int brd_dist_local_cols(int n, int b, int nranks, int rank);   /* n_loc of a rank (>= 0) */
+/* Stage 1 on the sharded matrix (every rank calls; BRD_DEVICE_PTR required). */
+int brd_ge2band_dist_f64(double *A_loc, int m, int n, int lda_loc, int b, unsigned flags);
+int brd_ge2band_dist_f32(float *A_loc, int m, int n, int lda_loc, int b, unsigned flags);
+/* Assemble the band (diagonals 0..b) on rank root into the dense m x n matrix
+ * B (device, ldb >= n; zero outside the band).  B is ignored on other ranks. */
+int brd_dist_gather_band_f64(const double *A_loc, int m, int n, int lda_loc, int b, double *B, int ldb, int root,
+                             unsigned flags);
+int brd_dist_gather_band_f32(const float *A_loc, int m, int n, int lda_loc, int b, float *B, int ldb, int root,
+                             unsigned flags);
 
 const char *brd_last_error(void);
 int brd_version(void);

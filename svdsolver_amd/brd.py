@@ -36,9 +36,15 @@ BRD_NO_EXTRACT = 0x8
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
     "brd_set_stream", "brd_use_own_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
-    "brd_dist_unique_id", "brd_dist_init", "brd_dist_finalize", "brd_last_error",
-    "brd_version",
+    "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
+    "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
+    "brd_last_error", "brd_version",
 )
+
+# brd_coll_fn (include/brd.h): int (*)(int op, const void *send, void *recv,
+#                                     unsigned long count, int dtype, int root, void *user)
+COLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 
 class BrdError(RuntimeError):
@@ -79,8 +85,19 @@ def _load() -> ctypes.CDLL:
     L.brd_dist_unique_id.restype = ci
     L.brd_dist_init.argtypes = [ci, ci, vp, ci]
     L.brd_dist_init.restype = ci
+    L.brd_dist_init_host.argtypes = [ci, ci, COLL_FN, vp]
+    L.brd_dist_init_host.restype = ci
     L.brd_dist_finalize.argtypes = []
     L.brd_dist_finalize.restype = ci
+    L.brd_dist_local_cols.argtypes = [ci, ci, ci, ci]
+    L.brd_dist_local_cols.restype = ci
+    for t in ("f64", "f32"):
+        f = getattr(L, f"brd_ge2band_dist_{t}")
+        f.argtypes = [vp, ci, ci, ci, ci, cu]
+        f.restype = ci
+        g = getattr(L, f"brd_dist_gather_band_{t}")
+        g.argtypes = [vp, ci, ci, ci, ci, vp, ci, ci, cu]
+        g.restype = ci
     L.brd_last_error.argtypes = []
     L.brd_last_error.restype = ctypes.c_char_p
     L.brd_version.argtypes = []

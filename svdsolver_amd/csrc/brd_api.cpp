@@ -226,7 +226,7 @@ static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sync, h
 }
 
 // Rows of every group of a tree level, summed (= rows touched by one apply).
-static long level_rows(const Tree &t, int level) {
+long tree_level_rows(const Tree &t, int level) {
     if (level == 0) return t.M;
     long r = 0;
     const int nprev = t.lv[level - 1].groups;
@@ -258,7 +258,7 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
         }
         if (n2 <= 0) continue;
         for (int l = 0; l < tq.nlevels; ++l) {
-            const double rows = (double)level_rows(tq, l);
+            const double rows = (double)tree_level_rows(tq, l);
             ProfScope ps("s1_apply", 4.0 * bk * rows * n2, 2.0 * rows * n2 * sizeof(T), s);
             HIP_TRY(launch_apply<T>(false, P + bk, lda, tq, l, n2, ws, s));
         }
@@ -274,13 +274,34 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
         const int m2 = m - k - bk;
         if (m2 <= 0) continue;
         for (int l = 0; l < tl.nlevels; ++l) {
-            const double rows = (double)level_rows(tl, l);
+            const double rows = (double)tree_level_rows(tl, l);
             ProfScope ps("s1_apply", 4.0 * bk * rows * m2, 2.0 * rows * m2 * sizeof(T), s);
             HIP_TRY(launch_apply<T>(true, Q + (long)bk * lda, lda, tl, l, m2, ws, s));
         }
     }
     return BRD_OK;
 }
+
+// --------------------------------------------------------------------------
+// services for the distributed driver (brd_internal.h)
+// --------------------------------------------------------------------------
+int api_fail(int code, const char *msg) { return fail(code, "%s", msg); }
+hipStream_t api_stream() { return stream(); }
+void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s) {
+    if (!g_ctx.prof) return nullptr;
+    Pending *p = new Pending{kind, get_event(), get_event(), flops, bytes};
+    hipEventRecord(p->a, s);
+    return p;
+}
+void api_prof_end(void *h, hipStream_t s) {
+    if (!h) return;
+    Pending *p = (Pending *)h;
+    hipEventRecord(p->b, s);
+    g_ctx.pending.push_back(*p);
+    delete p;
+}
+void api_lock() { g_ctx.mu.lock(); }
+void api_unlock() { g_ctx.mu.unlock(); }
 
 // --------------------------------------------------------------------------
 // host/device staging shared by both stages
@@ -431,14 +452,6 @@ int brd_profile_query(const char *kernel, long long *launches, double *total_ms,
     if (bytes) *bytes = a.bytes;
     return BRD_OK;
 }
-
-int brd_dist_unique_id(void *, int) {
-    return brd::fail(BRD_EUNSUPPORTED, "distributed stage 1 is not built yet");
-}
-int brd_dist_init(int, int, const void *, int) {
-    return brd::fail(BRD_EUNSUPPORTED, "distributed stage 1 is not built yet");
-}
-int brd_dist_finalize(void) { return BRD_OK; }
 
 const char *brd_last_error(void) { return brd::g_err.c_str(); }
 int brd_version(void) { return 1; }

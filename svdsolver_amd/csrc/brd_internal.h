@@ -62,4 +62,15 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *p
 template <typename T>
 hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStream_t s);
 
+// ---- services of the C-ABI layer (brd_api.cpp) used by the distributed
+// driver (brd_dist.hip) ------------------------------------------------------
+int api_fail(int code, const char *msg);           // sets brd_last_error, returns code
+hipStream_t api_stream();                          // the library stream
+void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
+void api_prof_end(void *handle, hipStream_t s);
+void api_lock();
+void api_unlock();
+// Stage-1 panel helpers shared with the single-GPU loop.
+long tree_level_rows(const Tree &t, int level);
+
 }  // namespace brd

@@ -1,0 +1,160 @@
+"""Multi-GPU stage 1 (block-cyclic column shards, svdsolver_amd/csrc/brd_dist.hip).
+
+CPU (gloo, world size 2 and 3): the layout helpers against the library's
+brd_dist_local_cols, and the distributed algorithm itself -- its numpy
+restatement tests/dist_sim.py, run as separate processes with the library's
+collectives through torch.distributed -- against the CPU oracle (|band|,
+the band is unique up to signs; fp64 normwise <= 1e-12).
+
+GPU: the library's distributed path with 2 and 3 ranks sharing cuda:0 through
+the host-callback communicator (gloo), and with RCCL at world size 1, against
+the single-GPU stage 1 (fp64 <= 1e-12, fp32 <= 1e-4 normwise on |band|) --
+RCCL cannot put two ranks on one GPU, so multi-rank RCCL runs only on a
+multi-GPU node (bench.py --gpus N).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _band_mask(n, b):
+    i, j = np.indices((n, n))
+    return (j >= i) & (j - i <= b)
+
+
+def _band_err(a, ref, b):
+    m = _band_mask(a.shape[0], b)
+    da = np.abs(a[m]).astype(np.float64) - np.abs(ref[m]).astype(np.float64)
+    return float(np.linalg.norm(da) / np.linalg.norm(ref[m].astype(np.float64)))
+
+
+# ---------------------------------------------------------------------------
+# layout (CPU)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n,b", [(64, 8), (100, 32), (1000, 32), (33, 32), (8192, 32)])
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+def test_local_cols_match_library(n, b, P):
+    from svdsolver_amd import dist, lib
+    tot = 0
+    for r in range(P):
+        nl = dist.local_cols(n, b, P, r)
+        assert nl == lib.brd_dist_local_cols(n, b, P, r)
+        assert nl == len(dist.global_columns(n, b, P, r))
+        tot += nl
+    assert tot == n
+
+
+def test_shard_roundtrip():
+    from svdsolver_amd import dist
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((70, 70))
+    for P in (1, 2, 3):
+        parts = [dist.shard(A, 8, P, r) for r in range(P)]
+        assert np.array_equal(dist.unshard(parts, 70, 8), A)
+
+
+# ---------------------------------------------------------------------------
+# the algorithm on CPU (gloo, separate processes)
+# ---------------------------------------------------------------------------
+def _sim_worker(rank, world, port, n, b, seed, out_path):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch.distributed as tdist
+    import dist_sim
+    from svdsolver_amd import dist
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    rng = np.random.default_rng(seed)
+    A = rng.uniform(1, 5, (n, n))
+    loc = dist.shard(A, b, world, rank).astype(np.float64)
+    dist_sim.ge2band_dist_sim(loc, n, b, rank, world, tdist)
+    import torch
+    wmax = max(dist.local_cols(n, b, world, r) for r in range(world))
+    mine = np.zeros((n, wmax))
+    mine[:, :loc.shape[1]] = loc
+    parts = [torch.zeros((n, wmax), dtype=torch.float64) for _ in range(world)]
+    tdist.all_gather(parts, torch.from_numpy(mine))
+    if rank == 0:
+        shards = [parts[r].numpy()[:, :dist.local_cols(n, b, world, r)] for r in range(world)]
+        np.save(out_path, dist.unshard(shards, n, b))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,b", [(2, 96, 8), (3, 100, 8), (2, 130, 32)])
+def test_distributed_algorithm_gloo(world, n, b, tmp_path):
+    import torch.multiprocessing as mp
+    from oracle import oracle
+    out = str(tmp_path / "band.npy")
+    mp.spawn(_sim_worker, args=(world, _free_port(), n, b, 3, out), nprocs=world, join=True)
+    band = np.load(out)
+    A = np.random.default_rng(3).uniform(1, 5, (n, n))
+    if n % b == 0:
+        ref = oracle.brd_p1(A, b)          # the reference's tiled algorithm needs b | n
+    else:
+        import dist_sim
+        ref = dist_sim.ge2band_dist_sim(A.copy(), n, b, 0, 1, dist_sim.LocalComm)
+    assert _band_err(band, ref, b) <= 1e-12
+    assert np.all(np.abs(band[~_band_mask(n, b)]) < 1e-12 * np.abs(ref).max())
+    # size-independent: the two-sided orthogonal reduction keeps the singular values
+    sa, sb = np.linalg.svd(A, compute_uv=False), np.linalg.svd(band, compute_uv=False)
+    assert np.max(np.abs(sa - sb)) <= 1e-12 * sa[0]
+
+
+# ---------------------------------------------------------------------------
+# the library's distributed path on the GPU
+# ---------------------------------------------------------------------------
+def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path):
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
+    import torch.distributed as tdist
+    from svdsolver_amd import dist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if mode == "rccl":
+        dist.init_rccl()
+    else:
+        dist.init_host()
+    rng = np.random.default_rng(5)
+    A = rng.uniform(1, 5, (n, n)).astype(dtype)
+    loc = torch.from_numpy(dist.shard(A, b, world, rank)).cuda()
+    dist.ge2band(loc, n, b)
+    B = dist.gather_band(loc, n, b, root=0)
+    if rank == 0:
+        np.save(out_path, B.cpu().numpy())
+    dist.finalize()
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,b,dtype,mode", [
+    (2, 640, 32, np.float64, "host"),
+    (3, 600, 32, np.float64, "host"),     # ragged last panel (600 = 18 * 32 + 24)
+    (2, 512, 16, np.float32, "host"),
+    (1, 512, 32, np.float64, "rccl"),
+])
+def test_distributed_stage1_gpu(world, n, b, dtype, mode, tmp_path):
+    import torch.multiprocessing as mp
+    import svdsolver_amd as S
+    out = str(tmp_path / "band.npy")
+    mp.spawn(_gpu_worker, args=(world, _free_port(), n, b, dtype, mode, out), nprocs=world, join=True)
+    band = np.load(out)
+    A = np.random.default_rng(5).uniform(1, 5, (n, n)).astype(dtype)
+    ref = S.brd_p1(A.astype(np.float64), b)
+    tol = 1e-12 if dtype == np.float64 else 1e-4
+    assert _band_err(band, ref, b) <= tol
+    assert np.all(band[~_band_mask(n, b)] == 0)

@@ -11,10 +11,13 @@ timed region, so no copy is timed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192] [--dtype f64] [--band 32]
 
-For N > 1 the driver launches one process per GPU (torch.distributed.run);
-each rank reduces its own matrices (replicas: the sharded stage 1 is not in
-this build, DESIGN.md "Multi-GPU"), the step time is the max over ranks and
-`value` is the aggregate GFLOP/s.
+For N > 1 the driver launches one process per GPU (torch.distributed.run).
+Default (--mode dist): ONE N x N matrix per step, its stage 1 sharded over
+the N GPUs (block-cyclic column panels, RCCL over xGMI, brd_ge2band_dist),
+the band gathered on rank 0 and stage 2 run there (it stays single-GPU,
+BASELINE.json north_star) -- strong scaling.  --mode replicas: every rank
+reduces its own matrices (weak scaling).  The step time is the max over ranks
+and `value` is the whole-job GFLOP/s.
 
 Rank 0 prints ONE JSON line.  Extra fields: the dominant kernel's roofline
 (HIP events around every k_apply launch, on the launch stream) and the CPU
@@ -48,6 +51,10 @@ def parse():
     p.add_argument("--band", type=int, default=32)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-n", type=int, default=1024)
+    p.add_argument("--mode", choices=["dist", "replicas"], default="dist",
+                   help="N > 1: sharded stage 1 of one matrix (dist) or independent replicas")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the distributed path even at world size 1 (launch through torch.distributed.run)")
     return p.parse_args()
 
 
@@ -96,7 +103,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_pg = world > 1 or args.force_dist
+    if use_pg:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -109,19 +117,39 @@ def main():
     n, b = args.n, args.band
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     nmat = args.warmup + args.steps
+    dist_mode = (world > 1 or args.force_dist) and args.mode == "dist"
+    stream = torch.cuda.current_stream(dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
-    mats = [base.clone() for _ in range(nmat)]
-    del base
-    stream = torch.cuda.current_stream(dev)
+    if dist_mode:
+        from svdsolver_amd import dist as D
+        D.init_rccl()
+        n_loc = D.local_cols(n, b, world, rank)
+        base = torch.rand((n, max(n_loc, 1)), dtype=tdt, device=dev, generator=g)[:, :n_loc] * 5.0
+        mats = [base.contiguous().clone() for _ in range(nmat)]
+        Bfull = torch.empty((n, n), dtype=tdt, device=dev) if rank == 0 else None
 
-    def step(A):
-        S.ge2band(A, b, sync=False)
-        S.band2bd(A, b, sync=False, extract=False)
+        def stage1(A):
+            D.ge2band(A, n, b, sync=False)
+            D.gather_band(A, n, b, root=0, out=Bfull, sync=False)
+
+        def stage2(A):
+            if rank == 0:
+                S.band2bd(Bfull, b, sync=False, extract=False)
+    else:
+        base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
+        mats = [base.clone() for _ in range(nmat)]
+
+        def stage1(A):
+            S.ge2band(A, b, sync=False)
+
+        def stage2(A):
+            S.band2bd(A, b, sync=False, extract=False)
+    del base
 
     for i in range(args.warmup):
-        step(mats[i])
+        stage1(mats[i])
+        stage2(mats[i])
     torch.cuda.synchronize(dev)
 
     S.profile_reset()
@@ -136,9 +164,9 @@ def main():
     for i in range(args.steps):
         A = mats[args.warmup + i]
         ev[i][0].record(stream)
-        S.ge2band(A, b, sync=False)
+        stage1(A)
         ev[i][1].record(stream)
-        S.band2bd(A, b, sync=False, extract=False)
+        stage2(A)
         ev[i][2].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -157,7 +185,8 @@ def main():
     sw = S.profile_query("s2_sweep")
 
     flops_per = 8.0 / 3.0 * n ** 3
-    value = world * args.steps * flops_per / elapsed / 1e9
+    matrices = 1 if (world == 1 or dist_mode) else world   # matrices reduced per step, whole job
+    value = matrices * args.steps * flops_per / elapsed / 1e9
     if rank == 0:
         ach = ap["flops"] / (ap["ms"] * 1e-3) / 1e12 if ap["ms"] > 0 else 0.0
         peak = PEAK_TFLOPS[args.dtype]
@@ -170,13 +199,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if (world > 1 and not dist_mode) else "strong",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic uniform [0,5) N x N, resident in HBM",
             "config": {"workload": f"two-stage bidiagonal reduction {n}x{n} {args.dtype}, band {b}, "
                                    f"stage 2 = reference window geometry (compat)",
-                       "n": n, "band": b, "global_batch": world, "parallelism": f"replicas{world}"},
+                       "n": n, "band": b, "global_batch": matrices,
+                       "parallelism": (f"stage1 block-cyclic columns over {world} GPUs (RCCL), stage2 rank 0"
+                                       if dist_mode else f"replicas{world}")},
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "roofline": {"kernel": "k_apply (stage-1 trailing update, MFMA)", "bound": "mfma",
                          "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
@@ -195,7 +226,9 @@ def main():
             except Exception as e:   # the baseline is reported, never required
                 out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_mode:
+        D.finalize()
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -40,10 +40,11 @@ __device__ unsigned long long g_s2stamps[kS2MaxBundles * kS2Stamp];
     do {                                                                         \
         if ((beta) < kS2MaxBundles) g_s2stamps[(beta) * kS2Stamp + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-// Per-bundle cycle accounting: [wave*3 + {0: wait prev sweep, 1: wait rows, 2: work}]
-// for compute waves 0..2, then loader {9: wait prev bundle, 10: wait ring, 11: load},
-// writer {12: wait fronts, 13: write}.
-constexpr int kS2Acc = 16;
+// Per-bundle cycle accounting, kept in registers and stored once per bundle
+// (a global update inside the loop would sit in the loader's vmcnt queue):
+// slots [4 * wave + j]: compute waves {0: wait prev sweep, 1: wait rows, 2: work},
+// loader {0: issue / poll, 1: wait landed}, writer {0: wait rows, 1: write}.
+constexpr int kS2Acc = 32;
 __device__ unsigned long long g_s2acc[kS2MaxBundles * kS2Acc];
 hipError_t read_s2stamps(unsigned long long *out, size_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2stamps), sizeof(unsigned long long) * n);
@@ -53,11 +54,16 @@ hipError_t read_s2acc(unsigned long long *out, size_t n) {
 }
 #define S2T0() const unsigned long long _t0 = __builtin_amdgcn_s_memtime()
 #define S2T(var) var = __builtin_amdgcn_s_memtime()
-#define S2ACC(beta, k, t0, t1) \
-    do { if ((beta) < kS2MaxBundles && lane == 0) g_s2acc[(beta) * kS2Acc + (k)] += (t1) - (t0); } while (0)
+#define S2ACC(beta, k, t0, t1) do { s2a[k] += (t1) - (t0); } while (0)
+#define S2FLUSH(beta)                                                                  \
+    do {                                                                               \
+        if ((beta) < kS2MaxBundles && lane == 0)                                       \
+            for (int j_ = 0; j_ < 4; ++j_) g_s2acc[(beta) * kS2Acc + 4 * wave + j_] += s2a[j_]; \
+    } while (0)
 #else
 #define S2STAMP(beta, k) do {} while (0)
 #define S2ACC(beta, k, t0, t1) do {} while (0)
+#define S2FLUSH(beta) do {} while (0)
 #endif
 #ifdef BRD_STAMPS
 #define S2CLK() __builtin_amdgcn_s_memtime()
@@ -493,6 +499,7 @@ struct BundleFlags {
     int front[16];   // top row of each wave's next window (n when done)
     int loaded;      // rows < loaded are in the ring (loader wave)
     int freed;       // ring slots of rows < freed may be reused (writer wave)
+    int avail;       // rows < avail have been written back by bundle beta-1 (poller wave)
 };
 
 __device__ __forceinline__ int lds_acq(const int *p) {
@@ -502,14 +509,15 @@ __device__ __forceinline__ void lds_rel(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// fp64 bundles are LDS-limited to S <= 3 compute waves (+ loader + writer),
-// which leaves the compute waves the registers of a 320-thread launch bound;
-// fp32 bundles to about 7, capped at 6 (512 threads, 256 VGPRs per wave).
+// Workgroup = S compute waves + loader + writer + poller.  fp64 bundles are
+// LDS-limited to S = 2 (the ring also needs slack for the loader, see
+// bundle_plan); fp32 to S = 5 (512 threads).
 template <typename T> constexpr int bundle_max_threads() { return sizeof(T) == 8 ? 320 : 512; }
-constexpr int kBankRows = 16;   // rows per loader register bank (two banks)
-constexpr int kWriteRows = 16;  // rows per writer iteration (at most)
+constexpr int kWriteRows = 16;  // rows per writer batch (at most)
+constexpr int kFly = 48;        // loader: rows in flight (LDS-DMA), <= 63
+constexpr int kChunk = 8;       // loader: rows published per wait
 
-// s_waitcnt vmcnt(k) for a run-time k in [0, 2 kWriteRows] (the immediate must be a constant)
+// s_waitcnt vmcnt(k) for a run-time k in [0, 48] (the immediate must be a constant)
 __device__ __forceinline__ void wait_vmcnt(int k) {
     switch (k) {
 #define BRD_VMCNT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
@@ -519,13 +527,15 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
         BRD_VMCNT_CASE(16) BRD_VMCNT_CASE(17) BRD_VMCNT_CASE(18) BRD_VMCNT_CASE(19) BRD_VMCNT_CASE(20)
         BRD_VMCNT_CASE(21) BRD_VMCNT_CASE(22) BRD_VMCNT_CASE(23) BRD_VMCNT_CASE(24) BRD_VMCNT_CASE(25)
         BRD_VMCNT_CASE(26) BRD_VMCNT_CASE(27) BRD_VMCNT_CASE(28) BRD_VMCNT_CASE(29) BRD_VMCNT_CASE(30)
-        BRD_VMCNT_CASE(31) BRD_VMCNT_CASE(32)
+        BRD_VMCNT_CASE(31) BRD_VMCNT_CASE(32) BRD_VMCNT_CASE(33) BRD_VMCNT_CASE(34) BRD_VMCNT_CASE(35)
+        BRD_VMCNT_CASE(36) BRD_VMCNT_CASE(37) BRD_VMCNT_CASE(38) BRD_VMCNT_CASE(39) BRD_VMCNT_CASE(40)
+        BRD_VMCNT_CASE(41) BRD_VMCNT_CASE(42) BRD_VMCNT_CASE(43) BRD_VMCNT_CASE(44) BRD_VMCNT_CASE(45)
+        BRD_VMCNT_CASE(46) BRD_VMCNT_CASE(47) BRD_VMCNT_CASE(48)
 #undef BRD_VMCNT_CASE
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
 template <typename T> constexpr int kEpp = 16 / sizeof(T);   // elements per 16-byte piece
-constexpr int kRsrcWord3 = 0x00020000;                       // raw buffer descriptor word 3 (gfx9 family)
 
 // Ring row pitch: diagonals -(b-1) .. 2b-1 (3b-1 elements), rounded up to a
 // multiple of 16 bytes (rows move as 16-byte pieces: LDS-DMA in, b128 out),
@@ -537,6 +547,32 @@ __host__ __device__ constexpr int ring_pitch(int b) {
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// One 16-byte piece per lane from global memory (sc1) straight into LDS at
+// lds_byte + 16 * lane (global_load_lds_dwordx4; M0 = the wave-uniform LDS base,
+// saved and restored inside the statement).  Counted by vmcnt; the compiler does
+// not see it, so the caller waits explicitly.
+__device__ __forceinline__ void dma16_sc1(const void *gsrc, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_byte) : "memory");
+}
+// Ring image of an edge row (some of its P columns outside the matrix):
+// clamped element loads, zeros outside.
+template <typename T>
+__device__ __forceinline__ void load_edge_row(const T *A, long lda, int n, int b, int r, T *dst, int row_q, int lane) {
+    if (lane < row_q) {
+        const int c0 = r - (b - 1) + lane * kEpp<T>;
+        T e[kEpp<T>];
+#pragma unroll
+        for (int k = 0; k < kEpp<T>; ++k) {
+            const int c = c0 + k;
+            e[k] = (c >= 0 && c < n) ? ld_c(A + (long)r * lda + c) : (T)0;
+        }
+        u32x4 v;
+        __builtin_memcpy(&v, e, 16);
+        *(u32x4 *)(dst + lane * kEpp<T>) = v;
+    }
+}
 // 16-byte agent-coherent (sc1, write-through) store
 __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
@@ -564,9 +600,12 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
             F->prog[threadIdx.x] = 0;
             F->front[threadIdx.x] = (int)threadIdx.x < nsw ? i0 + (int)threadIdx.x : n;
         }
-        if (threadIdx.x == 0) { F->loaded = i0; F->freed = i0; }
+        if (threadIdx.x == 0) { F->loaded = i0; F->freed = i0; F->avail = 0; }
         __syncthreads();
         if (threadIdx.x == 0) S2STAMP(beta, 0);
+#ifdef BRD_STAMPS
+        unsigned long long s2a[4] = {0, 0, 0, 0};
+#endif
 
         if (wave < nsw) {
             // ---------------- compute wave: sweep i0 + wave ----------------
@@ -588,14 +627,14 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                     }
                 }
                 unsigned long long c1 = S2CLK();
-                S2ACC(beta, wave * 3, c0, c1);
+                S2ACC(beta, 0, c0, c1);
                 if (live) {
                     while (lds_acq(&F->loaded) < wnd.i2) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 3); break; }
                     }
                     c0 = S2CLK();
-                    S2ACC(beta, wave * 3 + 1, c1, c0);
+                    S2ACC(beta, 1, c1, c0);
                     const int wr = wnd.i2 - wnd.i1, wc = wnd.j2 - wnd.j1;
                     if constexpr (KB > 0) {
                         if (right && wr == 2 * KB && wc == KB)
@@ -609,7 +648,7 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                         else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
                     }
                     c1 = S2CLK();
-                    S2ACC(beta, wave * 3 + 2, c0, c1);
+                    S2ACC(beta, 2, c0, c1);
                 }
                 if (lane == 0) {
                     lds_rel(&F->front[wave], it.next_top(t));
@@ -620,162 +659,128 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
             if (lane == 0 && wave == 0) S2STAMP(beta, 2);
             if (lane == 0 && wave == nsw - 1) S2STAMP(beta, 3);
         } else if (wave == S) {
-            // ---------------- loader wave: HBM -> registers -> ring ----------------
-            // Two register banks of kBankRows rows each (16-byte pieces, lane q
-            // holds piece q of every row) are fetched ahead with sc1 loads;
-            // when ring slots free up a bank is written with ds_write_b128 and
-            // refetched, so the ring's refill latency is an LDS latency, not an
-            // HBM round trip.  A bank is fetched only once bundle beta-1 has
-            // finished its rows (buffer loads with sc1; the compiler counts
-            // the outstanding loads, so the older bank is retired by a
-            // vmcnt(kBankRows) wait while the younger stays in flight).
+            // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
+            // An interior row (all P columns inside the matrix) is copied by ONE
+            // global_load_lds_dwordx4 (lane q moves 16-byte piece q, sc1) straight
+            // into its ring slot as soon as bundle beta-1 has written it back (the
+            // poller wave's `avail`) and its slot is free (`freed`).  Up to kFly
+            // rows are in flight; they are published (`loaded`) oldest first, at
+            // most kChunk at a time, behind counted vmcnt waits.  No vector load
+            // of this wave may sit between a DMA and its wait (the in-order vmcnt
+            // would drain every DMA in flight), so the flags come through LDS.
+            // Edge rows go synchronously through registers (clamped element
+            // loads, zeros outside the matrix).
             const int row_q = P * (int)sizeof(T) / 16;
-            const int *done_prev = beta > 0 ? rows_done + beta - 1 : nullptr;
-            int avail = done_prev ? __builtin_amdgcn_readfirstlane(ld_c(done_prev)) : n;
-            int spins = 0;
-            auto need_avail = [&](int hi) {      // wait until bundle beta-1 is done with rows < hi
-                hi = min(hi, n);
-                while (avail < hi) {
-                    __builtin_amdgcn_s_sleep(1);
-                    avail = __builtin_amdgcn_readfirstlane(ld_c(done_prev));
-                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 4); return false; }
-                }
-                return true;
-            };
-            auto fetch = [&](u32x4 (&bk)[kBankRows], int r0) {
-#pragma unroll
-                for (int rr = 0; rr < kBankRows; ++rr) {
-                    const int r = min(r0 + rr, n - 1);
-                    const int c0 = r - (b - 1) + (lane < row_q ? lane : 0) * kEpp<T>;
-                    // buffer descriptor at the row start (always inside the matrix), sc1
-                    const __amdgpu_buffer_rsrc_t rs =
-                        __builtin_amdgcn_make_buffer_rsrc((void *)(A + (long)r * lda), 0, 0x7fffffff, kRsrcWord3);
-                    // wave-uniform choice per row: exactly one load path runs, so
-                    // no load waits on another's destination registers
-                    if (r >= b - 1 && r - (b - 1) + P <= n) {
-                        bk[rr] = __builtin_amdgcn_raw_buffer_load_b128(rs, c0 * (int)sizeof(T), 0, 16);
-                    } else {
-                        // edge row: element loads at clamped columns (the columns
-                        // outside the matrix are zeroed when the bank is stored)
-                        T e[kEpp<T>];
-#pragma unroll
-                        for (int k = 0; k < kEpp<T>; ++k) {
-                            const int c = min(max(c0 + k, 0), n - 1);
-                            if constexpr (sizeof(T) == 8) {
-                                const auto w = __builtin_amdgcn_raw_buffer_load_b64(rs, c * 8, 0, 16);
-                                __builtin_memcpy(&e[k], &w, 8);
-                            } else {
-                                const auto w = __builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, 16);
-                                __builtin_memcpy(&e[k], &w, 4);
-                            }
-                        }
-                        __builtin_memcpy(&bk[rr], e, 16);
-                    }
-                }
-            };
-            auto store = [&](u32x4 (&bk)[kBankRows], int r0) {
-#pragma unroll
-                for (int rr = 0; rr < kBankRows; ++rr) {
-                    const int r = r0 + rr;
-                    if (r < n && lane < row_q) {
-                        const int c0 = r - (b - 1) + lane * kEpp<T>;
-                        u32x4 v = bk[rr];
-                        if (!(c0 >= 0 && c0 + kEpp<T> <= n)) {     // edge piece: zero outside the matrix
-                            T e[kEpp<T>];
-                            __builtin_memcpy(e, &v, 16);
-#pragma unroll
-                            for (int k = 0; k < kEpp<T>; ++k)
-                                if (c0 + k < 0 || c0 + k >= n) e[k] = (T)0;
-                            __builtin_memcpy(&v, e, 16);
-                        }
-                        *(u32x4 *)(ring + acc.slot(r) * P + lane * kEpp<T>) = v;
-                    }
-                }
-            };
-            auto need_ring = [&](int hi) {       // ring slots for rows < hi are free
-                hi = min(hi, n);
-                while (__builtin_amdgcn_readfirstlane(lds_acq(&F->freed)) + R < hi) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 6); return false; }
-                }
-                return true;
-            };
-            u32x4 bA[kBankRows], bB[kBankRows];
-            int ra = i0, rb = i0 + kBankRows;
+            const unsigned row_bytes = (unsigned)(P * (int)sizeof(T));
+            const unsigned ring_lds = (unsigned)(uintptr_t)ring;
+            const unsigned ring_end = ring_lds + (unsigned)R * row_bytes;
+            // rows [1, dma_hi] read P elements inside [A, A + (n-1) lda + n): DMA-able
+            const int dma_hi = (int)(((long)(n - 1) * lda + n + (b - 1) - P) / (lda + 1));
+            int ra = i0, rl = i0, spins = 0;
+            unsigned dst = ring_lds + (unsigned)acc.slot(i0) * row_bytes;   // slot of row ra
+            const char *src = (const char *)(A + (long)i0 * lda + i0 - (b - 1)) + 16 * lane;
+            const long rstep = (lda + 1) * (long)sizeof(T);
+            const bool dma_lane = lane < row_q;
             unsigned long long c0 = S2CLK();
-            bool ok = need_avail(ra + kBankRows);
-            fetch(bA, ra);
-            ok = ok && need_avail(rb + kBankRows);
-            fetch(bB, rb);
-            while (ok && ra < n) {
-                unsigned long long c1 = S2CLK();
-                S2ACC(beta, 9, c0, c1);
-                ok = need_ring(ra + kBankRows);
-                c0 = S2CLK();
-                S2ACC(beta, 10, c1, c0);
-                store(bA, ra);
-                if (lane == 0) lds_rel(&F->loaded, min(ra + kBankRows, n));
-                ra += 2 * kBankRows;
-                c1 = S2CLK();
-                S2ACC(beta, 11, c0, c1);
-                c0 = c1;
-                ok = ok && need_avail(ra + kBankRows);
-                fetch(bA, ra);
-                if (!ok || rb >= n) break;
-                c1 = S2CLK();
-                S2ACC(beta, 9, c0, c1);
-                ok = need_ring(rb + kBankRows);
-                c0 = S2CLK();
-                S2ACC(beta, 10, c1, c0);
-                store(bB, rb);
-                if (lane == 0) lds_rel(&F->loaded, min(rb + kBankRows, n));
-                rb += 2 * kBankRows;
-                c1 = S2CLK();
-                S2ACC(beta, 11, c0, c1);
-                c0 = c1;
-                ok = ok && need_avail(rb + kBankRows);
-                fetch(bB, rb);
+            while (rl < n) {
+                const int av = __hip_atomic_load(&F->avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int fr = __hip_atomic_load(&F->freed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int lim = __builtin_amdgcn_readfirstlane(min(min(av, fr + R), min(n, rl + kFly)));
+                bool moved = false;
+                if (ra < lim) {
+                    if (ra >= 1 && ra <= dma_hi) {
+                        const int stop = min(lim, dma_hi + 1);
+                        for (; ra < stop; ++ra) {
+                            if (dma_lane) dma16_sc1(src, dst);
+                            src += rstep;
+                            dst += row_bytes;
+                            if (dst == ring_end) dst = ring_lds;
+                        }
+                        moved = true;
+                    } else if (ra == rl) {   // edge row, once the DMAs before it have landed
+                        load_edge_row<T>(A, lda, n, b, ra, (T *)((char *)ring + (dst - ring_lds)), row_q, lane);
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        ++ra;
+                        rl = ra;
+                        src += rstep;
+                        dst += row_bytes;
+                        if (dst == ring_end) dst = ring_lds;
+                        if (lane == 0) lds_rel(&F->loaded, rl);
+                        moved = true;
+                    }
+                }
+                if (ra > rl) {
+                    unsigned long long c1 = S2CLK();
+                    S2ACC(beta, 0, c0, c1);
+                    const int keep = max(0, ra - rl - kChunk);
+                    wait_vmcnt(keep);
+                    rl = ra - keep;
+                    if (lane == 0) lds_rel(&F->loaded, rl);
+                    c0 = S2CLK();
+                    S2ACC(beta, 1, c1, c0);
+                    spins = 0;
+                } else if (!moved) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 4); break; }
+                }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) S2STAMP(beta, 5);
+        } else if (wave == S + 2) {
+            // ---------------- poller wave: rows bundle beta-1 has written back ----------------
+            if (beta == 0) {
+                if (lane == 0) lds_rel(&F->avail, n);
+            } else {
+                const int *done_prev = rows_done + beta - 1;
+                int av = 0, spins = 0;
+                while (av < n) {
+                    const int v = __builtin_amdgcn_readfirstlane(ld_c(done_prev));
+                    if (v != av) {
+                        av = v;
+                        if (lane == 0) lds_rel(&F->avail, v);
+                        spins = 0;
+                    } else {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 6); break; }
+                    }
+                }
+            }
         } else if (wave == S + 1) {
             // ---------------- writer wave: ring -> HBM ----------------
-            // Writes every row below all fronts (no sweep of the bundle touches
-            // it again), <= kWriteRows per iteration: ring -> registers (the
-            // slots are freed at once) -> 16-byte sc1 stores.  Store completion
-            // is pipelined two iterations deep: after issuing k stores, a
-            // vmcnt(k + k_prev) wait retires the iteration before the previous
-            // one, whose end row is then published in rows_done[beta].
+            // Writes every row below all fronts (no sweep of the bundle touches it
+            // again), <= kWriteRows per batch: ring -> registers (the slots are
+            // freed at once) -> 16-byte sc1 stores.  A batch is published in
+            // rows_done[beta] once its stores have drained, which the writer
+            // checks after issuing the next batch (counted vmcnt) or when idle,
+            // so the drain of one batch overlaps the next.
             const int row_q = P * (int)sizeof(T) / 16;
-            int wb = i0, spins = 0;
-            int pend0 = -1, pend1 = -1, k1 = 0;  // end rows of the two iterations in flight; stores of the younger
+            int wb = i0, spins = 0, pend = -1;
             unsigned long long c0 = S2CLK();
             while (wb < n) {
                 int fmin = n;
                 for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
                 const int wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_acq(&F->loaded)), wb + kWriteRows));
                 if (wt <= wb) {
-                    if (pend1 >= 0 || pend0 >= 0) {   // nothing new: retire everything in flight
+                    if (pend >= 0) {   // idle: retire the batch in flight
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0) st_c(rows_done + beta, pend1 >= 0 ? pend1 : pend0);
-                        pend0 = pend1 = -1;
-                        k1 = 0;
+                        if (lane == 0) st_c(rows_done + beta, pend);
+                        pend = -1;
+                        continue;
                     }
-                    const unsigned long long c1 = S2CLK();
-                    S2ACC(beta, 12, c0, c1);
-                    c0 = c1;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 5); break; }
                     continue;
                 }
                 spins = 0;
+                unsigned long long c1 = S2CLK();
+                S2ACC(beta, 0, c0, c1);
                 const int k = wt - wb;
                 u32x4 v[kWriteRows];
 #pragma unroll
                 for (int rr = 0; rr < kWriteRows; ++rr) {
                     const int r = min(wb + rr, wt - 1);
-                    const u32x4 *src = (const u32x4 *)(ring + acc.slot(r) * P);
-                    v[rr] = src[lane < row_q ? lane : 0];
+                    const u32x4 *srow = (const u32x4 *)(ring + acc.slot(r) * P);
+                    v[rr] = srow[lane < row_q ? lane : 0];
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (lane == 0) lds_rel(&F->freed, wt);   // slots reusable once read
@@ -783,50 +788,43 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                 if (interior) {
 #pragma unroll
                     for (int rr = 0; rr < kWriteRows; ++rr) {
-                        if (rr < k) {
-                            const int r = wb + rr;
-                            T *g = A + (long)r * lda + r - (b - 1);
-                            if (lane < row_q) st16_sc1((char *)g + 16 * lane, v[rr]);
-                        }
+                        const int r = wb + rr;
+                        if (rr < k && lane < row_q) st16_sc1(A + (long)r * lda + r - (b - 1) + lane * kEpp<T>, v[rr]);
                     }
-                    // retire everything but this iteration's and the previous one's stores
-                    wait_vmcnt(k + k1);
-                    if (pend0 >= 0 && lane == 0) st_c(rows_done + beta, pend0);
-                    pend0 = pend1;
-                    pend1 = wt;
-                    k1 = k;
+                    if (pend >= 0) {   // everything older than this batch's k stores has drained
+                        wait_vmcnt(k);
+                        if (lane == 0) st_c(rows_done + beta, pend);
+                    }
+                    pend = wt;
                 } else {
 #pragma unroll
                     for (int rr = 0; rr < kWriteRows; ++rr) {
                         const int r = wb + rr;
-                        if (r < wt && lane < row_q) {
+                        if (rr < k && lane < row_q) {
                             T *g = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
-                            const int c0 = r - (b - 1) + lane * kEpp<T>;
+                            const int cc0 = r - (b - 1) + lane * kEpp<T>;
                             T e[kEpp<T>];
                             __builtin_memcpy(e, &v[rr], 16);
 #pragma unroll
                             for (int kk = 0; kk < kEpp<T>; ++kk)
-                                if (c0 + kk >= 0 && c0 + kk < n) st_c(g + kk, e[kk]);
+                                if (cc0 + kk >= 0 && cc0 + kk < n) st_c(g + kk, e[kk]);
                         }
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) st_c(rows_done + beta, wt);
-                    pend0 = pend1 = -1;
-                    k1 = 0;
+                    pend = -1;
                 }
                 wb = wt;
-                {
-                    const unsigned long long c1 = S2CLK();
-                    S2ACC(beta, 13, c0, c1);
-                    c0 = c1;
-                }
+                c0 = S2CLK();
+                S2ACC(beta, 1, c1, c0);
             }
-            if (pend1 >= 0 || pend0 >= 0) {
+            if (pend >= 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) st_c(rows_done + beta, pend1 >= 0 ? pend1 : pend0);
+                if (lane == 0) st_c(rows_done + beta, pend);
             }
             if (lane == 0) S2STAMP(beta, 4);
         }
+        S2FLUSH(beta);
         __syncthreads();
     }
 }
@@ -856,16 +854,19 @@ template <typename T, bool EXACT>
 static bool bundle_plan(int n, int b, int &S, int &R) {
     const size_t budget = 160 * 1024 - 512;
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
-    int smax = EXACT ? 2 : bundle_max_threads<T>() / 64 - 2;
+    int smax = EXACT ? 2 : bundle_max_threads<T>() / 64 - 3;
     if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
-    for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
-        // + one loader bank: the loader hands rows over kBankRows at a time
-        const int rmin = ring_min_rows(b, S) + kBankRows;
-        if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
-            // largest ring that fits (more prefetch slack), but no more than n rows
-            R = rmin;
-            while (R < n + 1 && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
-            return true;
+    // Prefer the most sweeps whose ring keeps 2b rows of slack beyond the
+    // minimum (the loader's run-ahead); else the most that fit at all.
+    for (int slack : {2 * b, 8}) {
+        for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
+            const int rmin = ring_min_rows(b, S) + slack;
+            if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
+                // largest ring that fits, but no more than n rows
+                R = rmin;
+                while (R < n + 1 && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
+                return true;
+            }
         }
     }
     return false;
@@ -887,7 +888,7 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *p
     if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule (the loader assumes n >= 16 / sizeof(T))
         const int nbundles = (n - 1 + S - 1) / S;
         const int grid = std::max(1, std::min(nwaves, nbundles));
-        const dim3 block(64 * (S + 2));
+        const dim3 block(64 * (S + 3));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
         const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0>
                          : b == 32   ? (const void *)k_band2bd_bundle<T, false, 32>

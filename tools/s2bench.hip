@@ -27,25 +27,24 @@ int main(int argc, char **argv) {
         printf("stage2 n=%d: %.2f ms\n", n, ms);
         check_err("stage2");
     }
-    const int S = 3, nb = std::min(4096, (n - 1 + S - 1) / S);
+    const int S = 2, nb = std::min(4096, (n - 1 + S - 1) / S);
     std::vector<unsigned long long> st((size_t)nb * 6);
     (void)brd::read_s2stamps(st.data(), st.size());
-    unsigned long long t0 = st[0];
-    printf("beta   start   lead_t0   lead_done  trail_done  writer  loader   (us after bundle 0 start; clock ~100MHz?)\n");
-    for (int beta : {0, 1, 2, 3, 10, 100, 500, 1000, 2000, 2700}) {
+    printf("beta   lead_t0   lead_done  trail_done  writer  loader   (cycles after the bundle's start)\n");
+    for (int beta : {0, 1, 2, 3, 10, 100, 500, 1000, 2000, 3000, 4000}) {
         if (beta >= nb) continue;
         const unsigned long long *s = &st[(size_t)beta * 6];
-        printf("%5d %8lld %8lld %10lld %10lld %8lld %8lld\n", beta, (long long)(s[0] - t0), (long long)(s[1] - s[0]),
+        printf("%5d %8lld %10lld %10lld %8lld %8lld\n", beta, (long long)(s[1] - s[0]),
                (long long)(s[2] - s[0]), (long long)(s[3] - s[0]), (long long)(s[4] - s[0]), (long long)(s[5] - s[0]));
     }
-    std::vector<unsigned long long> ac((size_t)4096 * 16);
+    std::vector<unsigned long long> ac((size_t)4096 * 32);
     (void)brd::read_s2acc(ac.data(), ac.size());
-    printf("per-bundle cycles (accumulated over 2 runs): w0[prev,rows,work] w1[..] w2[..] loader[prev,ring,load] writer[wait,write]\n");
-    for (int beta : {0, 1, 2, 10, 100, 1000, 2000}) {
+    printf("per-bundle cycles (2 runs / 2): w0[prev,rows,work] w1[prev,rows,work] loader[issue,landed] writer[wait,write]\n");
+    for (int beta : {0, 1, 2, 10, 100, 1000, 2000, 3000}) {
         if (beta >= nb) continue;
-        printf("%5d", beta);
-        for (int k = 0; k < 14; ++k) printf(" %9llu", ac[(size_t)beta * 16 + k] / 2);
-        printf("\n");
+        const unsigned long long *a = &ac[(size_t)beta * 32];
+        printf("%5d  %9llu %9llu %9llu | %9llu %9llu %9llu | %9llu %9llu | %9llu %9llu\n", beta, a[0] / 2, a[1] / 2, a[2] / 2,
+               a[4] / 2, a[5] / 2, a[6] / 2, a[8] / 2, a[9] / 2, a[12] / 2, a[13] / 2);
     }
     return 0;
 }

@@ -1,0 +1,183 @@
+// Stage-2 window micro-benchmark (developer tool): one wave runs the interior
+// windows of a few sweeps on a band held in an LDS ring, timing each full
+// window with s_memtime.  Variant 0 = the production window code
+// (win_right_full / win_left_full), variant 1 = the candidate in this file.
+// Prints cycles per right / left window and the max difference of the bands.
+#include "../svdsolver_amd/csrc/brd_stage2.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+namespace brd {
+
+// ---------------- candidate window code ------------------------------------
+// 1/sqrt(q) and 1/u: hardware estimate + two Newton steps (full precision)
+__device__ __forceinline__ double rsq_nr(double q) {
+    double r = __builtin_amdgcn_rsq(q);
+    double h = 0.5 * q;
+    r = r * fma(-h * r, r, 1.5);
+    r = r * fma(-h * r, r, 1.5);
+    return r;
+}
+__device__ __forceinline__ double rcp_nr(double u) {
+    double y = __builtin_amdgcn_rcp(u);
+    y = fma(y, fma(-u, y, 1.0), y);
+    y = fma(y, fma(-u, y, 1.0), y);
+    return y;
+}
+// reflector of x applied to a (x[0] = the pivot): the norm and sigma = sum_{c>=1} a_c x_c
+// are accumulated together; alpha = 1/u1, tau = -s u1 / ||x||.
+template <int B>
+__device__ __forceinline__ void refl_apply_v1(double (&a)[B], const double (&x)[B]) {
+    double q[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
+    q[0] = x[0] * x[0];
+#pragma unroll
+    for (int c = 1; c < B; ++c) {
+        q[c & 3] = fma(x[c], x[c], q[c & 3]);
+        sg[c & 3] = fma(a[c], x[c], sg[c & 3]);
+    }
+    const double qq = (q[0] + q[1]) + (q[2] + q[3]);
+    const double sigma = (sg[0] + sg[1]) + (sg[2] + sg[3]);
+    const double rn = rsq_nr(qq);
+    const double nrm = qq * rn;
+    const double s = x[0] >= 0.0 ? -1.0 : 1.0;
+    const double u1 = fma(-s, nrm, x[0]);
+    const double alpha = rcp_nr(u1);
+    const double tau = -s * u1 * rn;
+    const double dot = fma(alpha, sigma, a[0]);
+    const double td = tau * dot;
+    a[0] -= td;
+    const double tda = td * alpha;
+#pragma unroll
+    for (int c = 1; c < B; ++c) a[c] = fma(-tda, x[c], a[c]);
+}
+
+template <typename T, int V, int B>
+__device__ __forceinline__ void win_right_v(const RingAcc<T> &A, int i1, int j1, int lane) {
+    if constexpr (V == 0) {
+        win_right_full<T, B>(A, i1, j1, lane);
+    } else {
+        const int r = i1 + (lane < 2 * B ? lane : 0);
+        const T *px = A.row(i1) + j1;
+        T *pa = A.row(r) + j1;
+        T a[B], x[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
+        refl_apply_v1<B>(a, x);
+        if (lane < 2 * B) {
+#pragma unroll
+            for (int c = 0; c < B; ++c) pa[c] = a[c];
+        }
+    }
+}
+template <typename T, int V, int B>
+__device__ __forceinline__ void win_left_v(const RingAcc<T> &A, int i1, int j1, int lane) {
+    if constexpr (V == 0) {
+        win_left_full<T, B>(A, i1, j1, lane);
+    } else {
+        const int col = lane < 2 * B ? lane : 0;
+        int slot = A.slot(i1);
+        T a[B], x[B];
+        T *rows[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) {
+            rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
+            x[r] = rows[r][0];
+            a[r] = rows[r][col];
+            slot = slot + 1 == A.R ? 0 : slot + 1;
+        }
+        refl_apply_v1<B>(a, x);
+        if (lane < 2 * B) {
+#pragma unroll
+            for (int r = 0; r < B; ++r) rows[r][col] = a[r];
+        }
+    }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(64) k_winbench(T *band, int n, int nsweeps, unsigned long long *out) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr int B = 32;
+    const int P = ring_pitch<T>(B);
+    T *ring = (T *)smem;
+    const int lane = threadIdx.x;
+    const RingAcc<T> acc{ring, P, n, B - 1, (unsigned)((0x100000000ull + n - 1) / n)};
+    for (int e = lane; e < n * P; e += 64) ring[e] = band[e];
+    __syncthreads();
+    unsigned long long cr = 0, cl = 0;
+    int nr = 0, nl = 0;
+    for (int i = 0; i < nsweeps; ++i) {
+        SweepIter it;
+        it.init(n, n, B, i);
+        for (int t = 0; t < it.ntask; ++t) {
+            bool right;
+            const Win w = it.task(t, right);
+            if (!(w.j2 > w.j1 && w.i2 > w.i1)) continue;
+            const int wr = w.i2 - w.i1, wc = w.j2 - w.j1;
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            if (right && wr == 2 * B && wc == B) {
+                win_right_v<T, V, B>(acc, w.i1, w.j1, lane);
+            } else if (!right && wr == B && wc == 2 * B) {
+                win_left_v<T, V, B>(acc, w.i1, w.j1, lane);
+            } else {
+                WaveLds<T, false> *S = nullptr;
+                __shared__ WaveLds<T, false> wl;
+                S = &wl;
+                if (right) win_right<T, false>(acc, w.i1, w.i2, w.j1, w.j2, *S, lane);
+                else       win_left<T, false>(acc, w.i1, w.i2, w.j1, w.j2, *S, lane);
+                continue;
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            if (right) { cr += t1 - t0; ++nr; } else { cl += t1 - t0; ++nl; }
+        }
+    }
+    __syncthreads();
+    for (int e = lane; e < n * P; e += 64) band[e] = ring[e];
+    if (lane == 0) { out[0] = cr; out[1] = nr; out[2] = cl; out[3] = nl; }
+}
+
+}  // namespace brd
+
+template <int V>
+static void run(const std::vector<double> &h0, int n, int nsw, std::vector<double> &res) {
+    const int P = brd::ring_pitch<double>(32);
+    double *d; unsigned long long *o;
+    (void)hipMalloc(&d, sizeof(double) * h0.size());
+    (void)hipMalloc(&o, 64);
+    (void)hipMemcpy(d, h0.data(), sizeof(double) * h0.size(), hipMemcpyHostToDevice);
+    const size_t lds = sizeof(double) * (size_t)n * P;
+    (void)hipFuncSetAttribute((const void *)brd::k_winbench<double, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((brd::k_winbench<double, V>), dim3(1), dim3(64), lds, 0, d, n, nsw, o);
+    unsigned long long ho[4];
+    (void)hipMemcpy(ho, o, 32, hipMemcpyDeviceToHost);
+    res.resize(h0.size());
+    (void)hipMemcpy(res.data(), d, sizeof(double) * h0.size(), hipMemcpyDeviceToHost);
+    const hipError_t e = hipGetLastError();
+    printf("variant %d: %s  right %.0f cyc (%llu)  left %.0f cyc (%llu)\n", V, hipGetErrorString(e),
+           (double)ho[0] / ho[1], ho[1], (double)ho[2] / ho[3], ho[3]);
+    (void)hipFree(d); (void)hipFree(o);
+}
+
+int main() {
+    const int n = 192, b = 32, P = brd::ring_pitch<double>(b), nsw = 8;
+    // ring image of a random band: row r at r*P, element (r, c) at offset c - r + b - 1
+    std::vector<double> h((size_t)n * P, 0.0);
+    unsigned long long s = 12345;
+    for (int r = 0; r < n; ++r)
+        for (int c = r; c <= std::min(n - 1, r + b); ++c) {
+            s = s * 6364136223846793005ull + 1442695040888963407ull;
+            h[(size_t)r * P + c - r + b - 1] = 1.0 + (double)(s >> 11) / 9007199254740992.0 * 4.0;
+        }
+    std::vector<double> r0, r1;
+    run<0>(h, n, nsw, r0);
+    run<1>(h, n, nsw, r1);
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < r0.size(); ++i) { md = std::max(md, std::fabs(r0[i] - r1[i])); mx = std::max(mx, std::fabs(r0[i])); }
+    printf("max |v0 - v1| = %.3e (max |v0| = %.3e)\n", md, mx);
+    return 0;
+}

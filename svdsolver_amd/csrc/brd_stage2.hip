@@ -46,6 +46,56 @@ __device__ unsigned long long g_s2stamps[kS2MaxBundles * kS2Stamp];
 // loader {0: issue / poll, 1: wait landed}, writer {0: wait rows, 1: write}.
 constexpr int kS2Acc = 32;
 __device__ unsigned long long g_s2acc[kS2MaxBundles * kS2Acc];
+// Cross-CU event times (s_memrealtime, 100 MHz, one clock for the whole chip)
+// for the hand-off of row X(beta) = beta*S + 300 from bundle beta to beta+1:
+// [beta][0] trail of beta moves its front past X, [beta][1] beta's writer
+// publishes rows_done > X, [beta+1][2] beta+1's poller sees it, [beta+1][3]
+// beta+1's loader publishes loaded > X, [beta+1][4] beta+1's lead starts the
+// first window that reaches row X.
+constexpr int kS2Ev = 8;
+__device__ unsigned long long g_s2ev[kS2MaxBundles * kS2Ev];
+hipError_t read_s2ev(unsigned long long *out, size_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2ev), sizeof(unsigned long long) * n);
+}
+#define S2EV(beta, k, cond)                                                                  \
+    do {                                                                                     \
+        if (!s2e[k] && (cond)) {                                                             \
+            s2e[k] = true;                                                                   \
+            if ((beta) < kS2MaxBundles) g_s2ev[(beta) * kS2Ev + (k)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                    \
+    } while (0)
+// Per-task timeline of bundles kTB0 and kTB0+1 (s_memrealtime): per compute
+// wave and task {start, ready (waits done), end}; and every publish of
+// {loaded, rows_done, avail} as (time, value).
+constexpr int kTB0 = 1000, kTT = 520, kPub = 2048;
+__device__ unsigned long long g_tt[2][4][kTT][3];
+__device__ unsigned long long g_pub[2][3][kPub][2];
+__device__ int g_npub[2][3];
+hipError_t reset_s2tt() {
+    static int z[2][3] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_npub), z, sizeof(z));
+}
+hipError_t read_s2tt(void *tt, void *pub, void *npub) {
+    hipError_t e = hipMemcpyFromSymbol(tt, HIP_SYMBOL(g_tt), sizeof(g_tt));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(pub, HIP_SYMBOL(g_pub), sizeof(g_pub));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(npub, HIP_SYMBOL(g_npub), sizeof(g_npub));
+    return e;
+}
+#define S2TT(beta, w, t, k)                                                                     \
+    do {                                                                                        \
+        if ((beta) >= kTB0 && (beta) < kTB0 + 2 && (t) < kTT && lane == 0)                      \
+            g_tt[(beta) - kTB0][w][t][k] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#define S2PUB(beta, kind, val)                                                                  \
+    do {                                                                                        \
+        if ((beta) >= kTB0 && (beta) < kTB0 + 2 && lane == 0) {                                  \
+            const int q_ = g_npub[(beta) - kTB0][kind]++;                                       \
+            if (q_ < kPub) {                                                                    \
+                g_pub[(beta) - kTB0][kind][q_][0] = __builtin_amdgcn_s_memrealtime();           \
+                g_pub[(beta) - kTB0][kind][q_][1] = (val);                                      \
+            }                                                                                   \
+        }                                                                                       \
+    } while (0)
 hipError_t read_s2stamps(unsigned long long *out, size_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2stamps), sizeof(unsigned long long) * n);
 }
@@ -62,6 +112,9 @@ hipError_t read_s2acc(unsigned long long *out, size_t n) {
     } while (0)
 #else
 #define S2STAMP(beta, k) do {} while (0)
+#define S2EV(beta, k, cond) do {} while (0)
+#define S2TT(beta, w, t, k) do {} while (0)
+#define S2PUB(beta, kind, val) do {} while (0)
 #define S2ACC(beta, k, t0, t1) do {} while (0)
 #define S2FLUSH(beta) do {} while (0)
 #endif
@@ -366,6 +419,142 @@ __device__ __forceinline__ void win_left_full(const RingAcc<T> &A, int i1, int j
     }
 }
 
+// ---- full interior windows split over a PAIR of waves (fast mode, B = 32) -----
+// Each wave takes half of the window with TWO lanes per row (right window) or
+// per column (left window), each lane holding B/2 elements, so a window's
+// per-lane work -- and its latency on the stage-2 critical path -- halves.
+// The two lanes of a row / column are neighbours (lane ^ 1): partial dot
+// products and norms are combined by one DPP swap.  Both waves form the
+// reflector redundantly from the shared source row / column.
+template <typename T>
+__device__ __forceinline__ T swap1(T v);   // value of lane ^ 1 (DPP quad_perm [1,0,3,2])
+template <>
+__device__ __forceinline__ double swap1<double>(double v) {
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0xB1, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, __double2loint(v), 0xB1, 0xf, 0xf, false));
+}
+template <>
+__device__ __forceinline__ float swap1<float>(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));
+}
+// 1/sqrt(q) and 1/u: hardware estimate refined by Newton steps to full precision
+__device__ __forceinline__ double rsq_nr(double q) {
+    double r = __builtin_amdgcn_rsq(q);
+    const double h = 0.5 * q;
+    r = r * fma(-h * r, r, 1.5);
+    r = r * fma(-h * r, r, 1.5);
+    return r;
+}
+__device__ __forceinline__ float rsq_nr(float q) {
+    float r = __builtin_amdgcn_rsqf(q);
+    return r * fmaf(-0.5f * q * r, r, 1.5f);
+}
+__device__ __forceinline__ double rcp_nr(double u) {
+    double y = __builtin_amdgcn_rcp(u);
+    y = fma(y, fma(-u, y, 1.0), y);
+    y = fma(y, fma(-u, y, 1.0), y);
+    return y;
+}
+__device__ __forceinline__ float rcp_nr(float u) {
+    const float y = __builtin_amdgcn_rcpf(u);
+    return fmaf(y, fmaf(-u, y, 1.0f), y);
+}
+// Apply the reflector of x (x0 = the pivot, element 0 of the source vector) to
+// a; this lane holds elements [h*H, h*H + H) of both (h = lane & 1).
+template <typename T, int H>
+__device__ __forceinline__ void refl_apply_pair(T (&a)[H], const T (&x)[H], T x0, int h) {
+    T q[4] = {(T)0, (T)0, (T)0, (T)0}, sg[4] = {(T)0, (T)0, (T)0, (T)0};
+#pragma unroll
+    for (int c = 0; c < H; ++c) q[c & 3] = fma(x[c], x[c], q[c & 3]);
+#pragma unroll
+    for (int c = 1; c < H; ++c) sg[c & 3] = fma(a[c], x[c], sg[c & 3]);
+    const T a0x0 = h ? a[0] * x[0] : (T)0;         // element 0 of the upper half is not the pivot
+    T qq = (q[0] + q[1]) + (q[2] + q[3]);
+    T sig = ((sg[0] + sg[1]) + (sg[2] + sg[3])) + a0x0;
+    qq += swap1(qq);
+    sig += swap1(sig);
+    const T a0o = swap1(a[0]);
+    const T a0 = h ? a0o : a[0];                     // the pivot-column element of this row / column
+    const T rn = rsq_nr(qq);
+    const T nrm = qq * rn;
+    const T sgn = x0 >= (T)0 ? (T)-1 : (T)1;
+    const T u1 = fma(-sgn, nrm, x0);
+    const T alpha = rcp_nr(u1);
+    const T tau = -sgn * u1 * rn;
+    const T td = tau * fma(alpha, sig, a0);
+    const T tda = td * alpha;
+    const T e0 = h ? fma(-tda, x[0], a[0]) : a[0] - td;
+#pragma unroll
+    for (int c = 1; c < H; ++c) a[c] = fma(-tda, x[c], a[c]);
+    a[0] = e0;
+}
+
+// right window rows [i1, i1+2B) x cols [j1, j1+B): this wave does rows
+// [i1 + half*B, i1 + half*B + B), lane -> row (lane >> 1), columns (lane & 1)*B/2 + [0, B/2)
+// The source row / column lies in half 0; the wave owning it (xo) must not
+// store before its partner has read the source: the partner raises its
+// x-flag (tag) once its loads have returned, the owner checks it before its
+// stores (PairSync).
+struct PairSync {
+    int *mine;            // this wave's x-flag
+    const int *partner;   // the partner's x-flag
+    int tag;
+    __device__ __forceinline__ void read_done(int lane) const {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(mine, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void before_store() const {
+        while (__hip_atomic_load(partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tag)
+            __builtin_amdgcn_s_sleep(0);
+    }
+};
+
+template <typename T, int B>
+__device__ __forceinline__ void win_right_pair(const RingAcc<T> &A, int i1, int j1, int half, int lane,
+                                               const PairSync &ps) {
+    constexpr int H = B / 2;
+    const int h = lane & 1;
+    const T *px = A.row(i1) + j1;
+    T *pa = A.row(i1 + half * B + (lane >> 1)) + j1 + h * H;
+    T a[H], x[H];
+#pragma unroll
+    for (int c = 0; c < H; ++c) { x[c] = px[h * H + c]; a[c] = pa[c]; }
+    const T x0 = px[0];
+    if (half != 0) ps.read_done(lane);
+    refl_apply_pair<T, H>(a, x, x0, h);
+    if (half == 0) ps.before_store();
+#pragma unroll
+    for (int c = 0; c < H; ++c) pa[c] = a[c];
+}
+
+// left window rows [i1, i1+B) x cols [j1, j1+2B): this wave does columns
+// [j1 + half*B, j1 + half*B + B), lane -> column (lane >> 1), rows (lane & 1)*B/2 + [0, B/2)
+template <typename T, int B>
+__device__ __forceinline__ void win_left_pair(const RingAcc<T> &A, int i1, int j1, int half, int lane,
+                                              const PairSync &ps) {
+    constexpr int H = B / 2;
+    const int h = lane & 1;
+    const int col = half * B + (lane >> 1);
+    const int s0 = A.slot(i1), s1 = A.slot(i1 + H);
+    int slot = h ? s1 : s0;
+    const int r0 = i1 + h * H;
+    T a[H], x[H];
+    T *rows[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        rows[k] = A.d + slot * A.P + A.off - (r0 + k) + j1;
+        x[k] = rows[k][0];
+        a[k] = rows[k][col];
+        slot = slot + 1 == A.R ? 0 : slot + 1;
+    }
+    const T x0 = A.row(i1)[j1];
+    if (half != 0) ps.read_done(lane);
+    refl_apply_pair<T, H>(a, x, x0, h);
+    if (half == 0) ps.before_store();
+#pragma unroll
+    for (int k = 0; k < H; ++k) rows[k][col] = a[k];
+}
+
 // ---- the reference's task list of one sweep --------------------------------
 // Task 0: top right window, task 1: top left window, then tasks 2+2k / 3+2k:
 // right / left windows of iteration k (svd_parallel.h:651-687).  An empty
@@ -500,6 +689,7 @@ struct BundleFlags {
     int loaded;      // rows < loaded are in the ring (loader wave)
     int freed;       // ring slots of rows < freed may be reused (writer wave)
     int avail;       // rows < avail have been written back by bundle beta-1 (poller wave)
+    int xr[16];      // wave pairs: the task (+1) whose reflector source this wave has read
 };
 
 __device__ __forceinline__ int lds_acq(const int *p) {
@@ -512,8 +702,13 @@ __device__ __forceinline__ void lds_rel(int *p, int v) {
 // Workgroup = S compute waves + loader + writer + poller.  fp64 bundles are
 // LDS-limited to S = 2 (the ring also needs slack for the loader, see
 // bundle_plan); fp32 to S = 5 (512 threads).
-template <typename T> constexpr int bundle_max_threads() { return sizeof(T) == 8 ? 320 : 512; }
-constexpr int kWriteRows = 16;  // rows per writer batch (at most)
+// W = compute waves per sweep: 2 on the b = 32 fast path (windows split over a
+// wave pair), else 1.
+template <bool EXACT, int KB> constexpr int bundle_w() { return (KB > 0 && !EXACT) ? 2 : 1; }
+template <typename T, int W> constexpr int bundle_max_threads() {
+    return sizeof(T) == 8 ? (W == 2 ? 512 : 320) : (W == 2 ? 1024 : 512);
+}
+constexpr int kWriteRows = 32;  // rows per writer batch (at most)
 constexpr int kFly = 48;        // loader: rows in flight (LDS-DMA), <= 63
 constexpr int kChunk = 8;       // loader: rows published per wait
 
@@ -578,9 +773,10 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <typename T, bool EXACT, int KB>
-__global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R,
-                                                         unsigned magic, int *rows_done, int *err)
+
+template <typename T, bool EXACT, int KB, int W>
+__global__ void __launch_bounds__((bundle_max_threads<T, W>()))
+k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int P = ring_pitch<T>(b);
@@ -598,32 +794,54 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
         const int nsw = min(S, n - 1 - i0);
         if (threadIdx.x < 16) {
             F->prog[threadIdx.x] = 0;
-            F->front[threadIdx.x] = (int)threadIdx.x < nsw ? i0 + (int)threadIdx.x : n;
+            F->xr[threadIdx.x] = 0;
+            F->front[threadIdx.x] = (int)threadIdx.x < W * nsw ? i0 + (int)threadIdx.x / W : n;
         }
         if (threadIdx.x == 0) { F->loaded = i0; F->freed = i0; F->avail = 0; }
         __syncthreads();
         if (threadIdx.x == 0) S2STAMP(beta, 0);
 #ifdef BRD_STAMPS
         unsigned long long s2a[4] = {0, 0, 0, 0};
+        bool s2e[5] = {false, false, false, false, false};
 #endif
 
-        if (wave < nsw) {
-            // ---------------- compute wave: sweep i0 + wave ----------------
-            const int i = i0 + wave;
+        if (wave < W * nsw) {
+            // ---------------- compute wave(s): sweep i0 + sw ----------------
+            // W = 2: waves 2sw (pw = 0) and 2sw + 1 (pw = 1) share the sweep; full
+            // windows are split between them (win_*_pair), the others run on
+            // wave pw = 0 alone.  Before task t a wave waits for its partner to
+            // finish task t - 1 (a window's reflector source comes from the
+            // partner's half of the previous window).
+            const int sw = wave / W, pw = wave - sw * W;
+            const int i = i0 + sw;
             SweepIter it;
             it.init(n, n, b, i);
-            const int prev_ntask = wave > 0 ? sweep_ntask(n, n, b, i - 1) : 0;
+            const int prev_ntask = sw > 0 ? sweep_ntask(n, n, b, i - 1) : 0;
             for (int t = 0; t < it.ntask; ++t) {
                 bool right;
                 const Win wnd = it.task(t, right);
                 const bool live = wnd.j2 > wnd.j1 && wnd.i2 > wnd.i1;
                 int spins = 0;
                 unsigned long long c0 = S2CLK();
-                if (wave > 0) {
+                S2TT(beta, wave, t, 0);
+                if (sw > 0) {
                     const int need = min(t + 4, prev_ntask);
-                    while (lds_acq(&F->prog[wave - 1]) < need) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
+                    if constexpr (W == 2) {
+                        while (min(lds_acq(&F->prog[2 * sw - 2]), lds_acq(&F->prog[2 * sw - 1])) < need) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
+                        }
+                    } else {
+                        while (lds_acq(&F->prog[sw - 1]) < need) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
+                        }
+                    }
+                }
+                if constexpr (W == 2) {
+                    while (lds_acq(&F->prog[wave ^ 1]) < t) {
+                        __builtin_amdgcn_s_sleep(0);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 7); break; }
                     }
                 }
                 unsigned long long c1 = S2CLK();
@@ -635,30 +853,44 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                     }
                     c0 = S2CLK();
                     S2ACC(beta, 1, c1, c0);
+                    if (lane == 0) S2EV(beta, 4, wave == 0 && wnd.i2 > (beta - 1) * S + 300);
+                    S2TT(beta, wave, t, 1);
                     const int wr = wnd.i2 - wnd.i1, wc = wnd.j2 - wnd.j1;
                     if constexpr (KB > 0) {
-                        if (right && wr == 2 * KB && wc == KB)
-                            win_right_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
-                        else if (!right && wr == KB && wc == 2 * KB)
-                            win_left_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
-                        else if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
-                        else            win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                        const bool full_r = right && wr == 2 * KB && wc == KB;
+                        const bool full_l = !right && wr == KB && wc == 2 * KB;
+                        if constexpr (W == 2) {
+                            const PairSync ps{&F->xr[wave], &F->xr[wave ^ 1], t + 1};
+                            if (full_r) win_right_pair<T, KB>(acc, wnd.i1, wnd.j1, pw, lane, ps);
+                            else if (full_l) win_left_pair<T, KB>(acc, wnd.i1, wnd.j1, 1 - pw, lane, ps);
+                            else if (pw == 0) {
+                                if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                                else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                            }
+                        } else {
+                            if (full_r) win_right_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
+                            else if (full_l) win_left_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
+                            else if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                            else            win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                        }
                     } else {
-                        if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
-                        else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[wave], lane);
+                        if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                        else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
                     }
                     c1 = S2CLK();
                     S2ACC(beta, 2, c0, c1);
                 }
+                S2TT(beta, wave, t, 2);
                 if (lane == 0) {
                     lds_rel(&F->front[wave], it.next_top(t));
                     lds_rel(&F->prog[wave], t + 1);
+                    S2EV(beta, 0, wave == W * nsw - 1 && it.next_top(t) > beta * S + 300);
                     if (wave == 0 && t == 0) S2STAMP(beta, 1);
                 }
             }
             if (lane == 0 && wave == 0) S2STAMP(beta, 2);
-            if (lane == 0 && wave == nsw - 1) S2STAMP(beta, 3);
-        } else if (wave == S) {
+            if (lane == 0 && wave == W * nsw - 1) S2STAMP(beta, 3);
+        } else if (wave == W * S) {
             // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
             // An interior row (all P columns inside the matrix) is copied by ONE
             // global_load_lds_dwordx4 (lane q moves 16-byte piece q, sc1) straight
@@ -716,6 +948,8 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                     wait_vmcnt(keep);
                     rl = ra - keep;
                     if (lane == 0) lds_rel(&F->loaded, rl);
+                    if (lane == 0) S2EV(beta, 3, rl > (beta - 1) * S + 300);
+                    S2PUB(beta, 0, rl);
                     c0 = S2CLK();
                     S2ACC(beta, 1, c1, c0);
                     spins = 0;
@@ -726,7 +960,7 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) S2STAMP(beta, 5);
-        } else if (wave == S + 2) {
+        } else if (wave == W * S + 2) {
             // ---------------- poller wave: rows bundle beta-1 has written back ----------------
             if (beta == 0) {
                 if (lane == 0) lds_rel(&F->avail, n);
@@ -738,6 +972,8 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                     if (v != av) {
                         av = v;
                         if (lane == 0) lds_rel(&F->avail, v);
+                        if (lane == 0) S2EV(beta, 2, v > (beta - 1) * S + 300);
+                        S2PUB(beta, 2, v);
                         spins = 0;
                     } else {
                         __builtin_amdgcn_s_sleep(1);
@@ -745,7 +981,7 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                     }
                 }
             }
-        } else if (wave == S + 1) {
+        } else if (wave == W * S + 1) {
             // ---------------- writer wave: ring -> HBM ----------------
             // Writes every row below all fronts (no sweep of the bundle touches it
             // again), <= kWriteRows per batch: ring -> registers (the slots are
@@ -758,12 +994,14 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
             unsigned long long c0 = S2CLK();
             while (wb < n) {
                 int fmin = n;
-                for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
+                for (int s = 0; s < W * nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
                 const int wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_acq(&F->loaded)), wb + kWriteRows));
                 if (wt <= wb) {
                     if (pend >= 0) {   // idle: retire the batch in flight
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         if (lane == 0) st_c(rows_done + beta, pend);
+                        if (lane == 0) S2EV(beta, 1, pend > beta * S + 300);
+                        S2PUB(beta, 1, pend);
                         pend = -1;
                         continue;
                     }
@@ -776,24 +1014,37 @@ __global__ void __launch_bounds__(bundle_max_threads<T>()) k_band2bd_bundle(T *A
                 S2ACC(beta, 0, c0, c1);
                 const int k = wt - wb;
                 u32x4 v[kWriteRows];
+                {
+                    int sl = acc.slot(wb);
+                    const u32x4 *srow = (const u32x4 *)(ring + sl * P) + (lane < row_q ? lane : 0);
+                    const int wrap = R - sl;   // rows before the ring wraps
 #pragma unroll
-                for (int rr = 0; rr < kWriteRows; ++rr) {
-                    const int r = min(wb + rr, wt - 1);
-                    const u32x4 *srow = (const u32x4 *)(ring + acc.slot(r) * P);
-                    v[rr] = srow[lane < row_q ? lane : 0];
+                    for (int rr = 0; rr < kWriteRows; ++rr) {
+                        if (rr < k) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
+                    }
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (lane == 0) lds_rel(&F->freed, wt);   // slots reusable once read
                 const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
                 if (interior) {
+                    if (lane < row_q) {
+                        const char *g = (const char *)(A + (long)wb * lda + wb - (b - 1)) + 16 * lane;
+                        const long gstep = (lda + 1) * (long)sizeof(T);
 #pragma unroll
-                    for (int rr = 0; rr < kWriteRows; ++rr) {
-                        const int r = wb + rr;
-                        if (rr < k && lane < row_q) st16_sc1(A + (long)r * lda + r - (b - 1) + lane * kEpp<T>, v[rr]);
+                        for (int rr = 0; rr < kWriteRows; ++rr) {
+                            if (rr < k) st16_sc1((void *)g, v[rr]);
+                            g += gstep;
+                        }
                     }
                     if (pend >= 0) {   // everything older than this batch's k stores has drained
+                        unsigned long long c2 = S2CLK();
+                        S2ACC(beta, 2, c1, c2);
                         wait_vmcnt(k);
+                        c1 = S2CLK();
+                        S2ACC(beta, 3, c2, c1);
                         if (lane == 0) st_c(rows_done + beta, pend);
+                        if (lane == 0) S2EV(beta, 1, pend > beta * S + 300);
+                        S2PUB(beta, 1, pend);
                     }
                     pend = wt;
                 } else {
@@ -850,11 +1101,11 @@ static size_t bundle_lds_bytes(int b, int S, int R) {
     return ring + (size_t)S * sizeof(WaveLds<T, EXACT>) + sizeof(BundleFlags);
 }
 
-template <typename T, bool EXACT>
+template <typename T, bool EXACT, int W>
 static bool bundle_plan(int n, int b, int &S, int &R) {
     const size_t budget = 160 * 1024 - 512;
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
-    int smax = EXACT ? 2 : bundle_max_threads<T>() / 64 - 3;
+    int smax = EXACT ? 2 : (bundle_max_threads<T, W>() / 64 - 3) / W;
     if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
     // Prefer the most sweeps whose ring keeps 2b rows of slack beyond the
     // minimum (the loader's run-ahead); else the most that fit at all.
@@ -884,24 +1135,32 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *p
     static const char *sel = getenv("BRD_S2_SCHEDULE");   // "pipe" selects the HBM-only schedule
     const bool pipe = sel && sel[0] == 'p';
     int S = 0, R = 0;
-    const bool ok = exact_order ? bundle_plan<T, true>(n, b, S, R) : bundle_plan<T, false>(n, b, S, R);
-    if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule (the loader assumes n >= 16 / sizeof(T))
+    const bool fast32 = !exact_order && b == 32;
+    static const char *penv = getenv("BRD_S2_PAIR");    // tuning: "1" = wave pairs per sweep on the b = 32 path
+    const int W = fast32 && penv && penv[0] == '1' ? 2 : 1;
+    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, S, R)
+                    : W == 2    ? bundle_plan<T, false, 2>(n, b, S, R)
+                                : bundle_plan<T, false, 1>(n, b, S, R);
+    if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule
         const int nbundles = (n - 1 + S - 1) / S;
         const int grid = std::max(1, std::min(nwaves, nbundles));
-        const dim3 block(64 * (S + 3));
+        const dim3 block(64 * (W * S + 3));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
-        const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0>
-                         : b == 32   ? (const void *)k_band2bd_bundle<T, false, 32>
-                                     : (const void *)k_band2bd_bundle<T, false, 0>;
+        const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0, 1>
+                         : W == 2    ? (const void *)k_band2bd_bundle<T, false, 32, 2>
+                         : fast32    ? (const void *)k_band2bd_bundle<T, false, 32, 1>
+                                     : (const void *)k_band2bd_bundle<T, false, 0, 1>;
         const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
-        else if (b == 32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+        else if (W == 2)
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+        else if (fast32)
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const int grid = std::max(1, std::min(nwaves, n - 1));

@@ -6,7 +6,7 @@
 #include <cstdio>
 #include <vector>
 #include "brd_internal.h"
-namespace brd { hipError_t read_s2stamps(unsigned long long *out, size_t n); hipError_t read_s2acc(unsigned long long *out, size_t n); }
+namespace brd { hipError_t read_s2stamps(unsigned long long *out, size_t n); hipError_t read_s2acc(unsigned long long *out, size_t n); hipError_t read_s2ev(unsigned long long *out, size_t n); hipError_t reset_s2tt(); hipError_t read_s2tt(void *tt, void *pub, void *npub); }
 static void check_err(const char *what) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e)); exit(3); }
@@ -18,8 +18,10 @@ int main(int argc, char **argv) {
     for (int i = 0; i < n; ++i) for (int j = i; j <= std::min(n - 1, i + b); ++j) h[(size_t)i * n + j] = 1.0 + ((i * 31 + j * 17) % 97) / 97.0;
     int *flags; (void)hipMalloc(&flags, sizeof(int) * (n + 2));
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    std::vector<unsigned long long> zero((size_t)4096 * 8, 0ull);
     for (int it = 0; it < 2; ++it) {
         (void)hipMemcpy(A, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice);
+        (void)brd::reset_s2tt();
         (void)hipEventRecord(e0);
         (void)brd::launch_band2bd<double>(A, n, n, b, false, flags, flags + n + 1, 256, 0);
         (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
@@ -39,12 +41,31 @@ int main(int argc, char **argv) {
     }
     std::vector<unsigned long long> ac((size_t)4096 * 32);
     (void)brd::read_s2acc(ac.data(), ac.size());
-    printf("per-bundle cycles (2 runs / 2): w0[prev,rows,work] w1[prev,rows,work] loader[issue,landed] writer[wait,write]\n");
+    printf("per-bundle cycles (2 runs / 2): compute waves [prev,rows,work] x4 | loader[issue,landed] writer[wait,write]\n");
     for (int beta : {0, 1, 2, 10, 100, 1000, 2000, 3000}) {
         if (beta >= nb) continue;
         const unsigned long long *a = &ac[(size_t)beta * 32];
-        printf("%5d  %9llu %9llu %9llu | %9llu %9llu %9llu | %9llu %9llu | %9llu %9llu\n", beta, a[0] / 2, a[1] / 2, a[2] / 2,
-               a[4] / 2, a[5] / 2, a[6] / 2, a[8] / 2, a[9] / 2, a[12] / 2, a[13] / 2);
+        printf("%5d ", beta);
+        for (int w = 0; w < 4; ++w) printf(" %8llu %8llu %8llu |", a[4 * w] / 2, a[4 * w + 1] / 2, a[4 * w + 2] / 2);
+        printf(" %8llu %8llu | %8llu %8llu [issue %llu drain %llu]\n", a[16] / 2, a[17] / 2, a[20] / 2, a[21] / 2, a[22] / 2, a[23] / 2);
+    }
+    {
+        std::vector<unsigned long long> ev((size_t)4096 * 8);
+        (void)brd::read_s2ev(ev.data(), ev.size());
+        printf("hand-off of row beta*S+300 (us, from the trail's front passing it): writer-published poller-seen loader-loaded lead-uses  | next bundle's t0 lag\n");
+        for (int beta : {1, 2, 3, 10, 100, 500, 1000, 2000, 3000}) {
+            if (beta + 1 >= nb) continue;
+            const unsigned long long *e0 = &ev[(size_t)beta * 8], *e1 = &ev[(size_t)(beta + 1) * 8];
+            auto us = [&](unsigned long long x) { return x ? (double)((long long)(x - e0[0])) / 100.0 : -1.0; };
+            printf("%5d  %8.2f %8.2f %8.2f %8.2f\n", beta, us(e0[1]), us(e1[2]), us(e1[3]), us(e1[4]));
+        }
+    }
+    {
+        static unsigned long long tt[2][4][520][3], pub[2][3][2048][2];
+        static int npub[2][3];
+        (void)brd::read_s2tt(tt, pub, npub);
+        FILE *f = fopen("gpurun_out/s2tt.bin", "wb");
+        if (f) { fwrite(tt, sizeof(tt), 1, f); fwrite(pub, sizeof(pub), 1, f); fwrite(npub, sizeof(npub), 1, f); fclose(f); }
     }
     return 0;
 }

@@ -53,10 +53,31 @@ __device__ __forceinline__ void refl_apply_v1(double (&a)[B], const double (&x)[
     for (int c = 1; c < B; ++c) a[c] = fma(-tda, x[c], a[c]);
 }
 
+__device__ unsigned long long g_ph[8];
 template <typename T, int V, int B>
 __device__ __forceinline__ void win_right_v(const RingAcc<T> &A, int i1, int j1, int lane) {
     if constexpr (V == 0) {
         win_right_full<T, B>(A, i1, j1, lane);
+    } else if constexpr (V == 2) {
+        const int r = i1 + (lane < 2 * B ? lane : 0);
+        const T *px = A.row(i1) + j1;
+        T *pa = A.row(r) + j1;
+        T a[B], x[B];
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        refl_apply_v1<B>(a, x);
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        if (lane < 2 * B) {
+#pragma unroll
+            for (int c = 0; c < B; ++c) pa[c] = a[c];
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) { g_ph[0] += t1 - t0; g_ph[1] += t2 - t1; g_ph[2] += t3 - t2; g_ph[3] += 1; }
     } else {
         const int r = i1 + (lane < 2 * B ? lane : 0);
         const T *px = A.row(i1) + j1;
@@ -75,6 +96,31 @@ template <typename T, int V, int B>
 __device__ __forceinline__ void win_left_v(const RingAcc<T> &A, int i1, int j1, int lane) {
     if constexpr (V == 0) {
         win_left_full<T, B>(A, i1, j1, lane);
+    } else if constexpr (V == 2) {
+        const int col = lane < 2 * B ? lane : 0;
+        int slot = A.slot(i1);
+        T a[B], x[B];
+        T *rows[B];
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int r = 0; r < B; ++r) {
+            rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
+            x[r] = rows[r][0];
+            a[r] = rows[r][col];
+            slot = slot + 1 == A.R ? 0 : slot + 1;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        refl_apply_v1<B>(a, x);
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        if (lane < 2 * B) {
+#pragma unroll
+            for (int r = 0; r < B; ++r) rows[r][col] = a[r];
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) { g_ph[4] += t1 - t0; g_ph[5] += t2 - t1; g_ph[6] += t3 - t2; g_ph[7] += 1; }
     } else {
         const int col = lane < 2 * B ? lane : 0;
         int slot = A.slot(i1);
@@ -173,9 +219,14 @@ int main() {
             s = s * 6364136223846793005ull + 1442695040888963407ull;
             h[(size_t)r * P + c - r + b - 1] = 1.0 + (double)(s >> 11) / 9007199254740992.0 * 4.0;
         }
-    std::vector<double> r0, r1;
+    std::vector<double> r0, r1, r2;
     run<0>(h, n, nsw, r0);
     run<1>(h, n, nsw, r1);
+    run<2>(h, n, nsw, r2);
+    unsigned long long ph[8];
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(brd::g_ph), sizeof(ph));
+    printf("phases right: load %.0f compute %.0f store %.0f | left: load %.0f compute %.0f store %.0f\n",
+           (double)ph[0] / ph[3], (double)ph[1] / ph[3], (double)ph[2] / ph[3], (double)ph[4] / ph[7], (double)ph[5] / ph[7], (double)ph[6] / ph[7]);
     double md = 0, mx = 0;
     for (size_t i = 0; i < r0.size(); ++i) { md = std::max(md, std::fabs(r0[i] - r1[i])); mx = std::max(mx, std::fabs(r0[i])); }
     printf("max |v0 - v1| = %.3e (max |v0| = %.3e)\n", md, mx);

@@ -101,6 +101,8 @@ struct Ctx {
     bool have_user_stream = false;   // true: use user_stream (NULL = legacy default stream)
     hipStream_t user_stream = nullptr;
     hipStream_t own_stream = nullptr;
+    hipStream_t side_stream = nullptr;   // stage 1: root-level factors beside the leaf apply
+    hipEvent_t ev_leaf = nullptr, ev_root = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0;
     int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
@@ -117,6 +119,15 @@ static hipStream_t stream() {
     if (g_ctx.have_user_stream) return g_ctx.user_stream;
     if (!g_ctx.own_stream) hipStreamCreateWithFlags(&g_ctx.own_stream, hipStreamNonBlocking);
     return g_ctx.own_stream;
+}
+
+static int ensure_side() {
+    if (g_ctx.side_stream) return BRD_OK;
+    if (hipStreamCreateWithFlags(&g_ctx.side_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g_ctx.ev_leaf, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g_ctx.ev_root, hipEventDisableTiming) != hipSuccess)
+        return fail(BRD_EHIP, "stage-1 side stream / events could not be created");
+    return BRD_OK;
 }
 
 static int ensure_ws(size_t bytes) {
@@ -237,11 +248,52 @@ long tree_level_rows(const Tree &t, int level) {
 // --------------------------------------------------------------------------
 // stage 1 panel loop on a device matrix
 // --------------------------------------------------------------------------
+// One side (QR of a column panel + left update, or LQ of a row panel + right
+// update) of panel k.  The reduction tree's upper levels depend only on the
+// leaves' R factors (panel columns) and the leaf-level apply only on the
+// leaves' V, T (trailing columns), so the upper-level factors run on the side
+// stream while the leaf apply runs on the main stream; the upper-level applies
+// wait for both.
+template <typename T>
+static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &ws, T *X, int ncols,
+                      hipStream_t s) {
+    {
+        ProfScope ps("s1_factor", 0, 0, s);
+        HIP_TRY(launch_factor<T>(trans, P, lda, t, 0, ws, s));
+    }
+    static const char *ov = getenv("BRD_S1_OVERLAP");   // tuning: "0" = no side stream
+    const bool split = t.nlevels > 1 && ncols > 0 && !(ov && ov[0] == '0');
+    if (split) {
+        HIP_TRY(hipEventRecord(g_ctx.ev_leaf, s));
+        HIP_TRY(hipStreamWaitEvent(g_ctx.side_stream, g_ctx.ev_leaf, 0));
+    }
+    hipStream_t sf = split ? g_ctx.side_stream : s;
+    for (int l = 1; l < t.nlevels; ++l) {
+        ProfScope ps("s1_factor", 0, 0, sf);
+        HIP_TRY(launch_factor<T>(trans, P, lda, t, l, ws, sf));
+    }
+    if (ncols <= 0) return BRD_OK;
+    for (int l = 0; l < t.nlevels; ++l) {
+        if (l == 1 && split) {
+            HIP_TRY(hipEventRecord(g_ctx.ev_root, sf));
+            HIP_TRY(hipStreamWaitEvent(s, g_ctx.ev_root, 0));
+        }
+        const double rows = (double)tree_level_rows(t, l);
+        ProfScope ps("s1_apply", 4.0 * t.bk * rows * ncols, 2.0 * rows * ncols * sizeof(T), s);
+        static const char *fe = getenv("BRD_S1_FREE");   // tuning: CUs left free beside the leaf apply
+        const int free_cus = fe ? atoi(fe) : 16;
+        HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, l == 0 && split ? 256 - free_cus : 256));
+    }
+    return BRD_OK;
+}
+
 template <typename T>
 static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
     int rc = ensure_ws(need);
+    if (rc) return rc;
+    rc = ensure_side();
     if (rc) return rc;
     TreeWs ws;
     for (int k = 0; k < n; k += b) {
@@ -249,35 +301,19 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
         const int mp = m - k;
         const int n2 = n - k - bk;
         T *P = A + (long)k * lda + k;
-        // ---- QR of the column panel A[k:m, k:k+bk], left update of A[k:m, k+bk:n]
+        // QR of the column panel A[k:m, k:k+bk], left update of A[k:m, k+bk:n]
         const Tree tq = make_tree(mp, bk);
         tree_ws_carve(tq, sizeof(T), g_ctx.ws, ws);
-        for (int l = 0; l < tq.nlevels; ++l) {
-            ProfScope ps("s1_factor", 0, 0, s);
-            HIP_TRY(launch_factor<T>(false, P, lda, tq, l, ws, s));
-        }
+        rc = panel_side<T>(false, P, lda, tq, ws, P + bk, n2, s);
+        if (rc) return rc;
         if (n2 <= 0) continue;
-        for (int l = 0; l < tq.nlevels; ++l) {
-            const double rows = (double)tree_level_rows(tq, l);
-            ProfScope ps("s1_apply", 4.0 * bk * rows * n2, 2.0 * rows * n2 * sizeof(T), s);
-            HIP_TRY(launch_apply<T>(false, P + bk, lda, tq, l, n2, ws, s));
-        }
-        // ---- LQ of the row panel A[k:k+bk, k+bk:n] (logical transpose),
-        //      right update of A[k+bk:m, k+bk:n]
+        // LQ of the row panel A[k:k+bk, k+bk:n] (logical transpose), right
+        // update of A[k+bk:m, k+bk:n]
         const Tree tl = make_tree(n2, bk);
         tree_ws_carve(tl, sizeof(T), g_ctx.ws, ws);
         T *Q = P + bk;
-        for (int l = 0; l < tl.nlevels; ++l) {
-            ProfScope ps("s1_factor", 0, 0, s);
-            HIP_TRY(launch_factor<T>(true, Q, lda, tl, l, ws, s));
-        }
-        const int m2 = m - k - bk;
-        if (m2 <= 0) continue;
-        for (int l = 0; l < tl.nlevels; ++l) {
-            const double rows = (double)tree_level_rows(tl, l);
-            ProfScope ps("s1_apply", 4.0 * bk * rows * m2, 2.0 * rows * m2 * sizeof(T), s);
-            HIP_TRY(launch_apply<T>(true, Q + (long)bk * lda, lda, tl, l, m2, ws, s));
-        }
+        rc = panel_side<T>(true, Q, lda, tl, ws, Q + (long)bk * lda, m - k - bk, s);
+        if (rc) return rc;
     }
     return BRD_OK;
 }

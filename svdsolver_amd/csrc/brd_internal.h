@@ -51,9 +51,11 @@ void tree_ws_carve(const Tree &t, size_t elem, void *base, TreeWs &ws);
 template <typename T>
 hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
                          const TreeWs &ws, hipStream_t s);
+// target: workgroups to aim for (about one per CU; fewer leaves CUs free for
+// a factor kernel running beside the apply).
 template <typename T>
 hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
-                        int ncols, const TreeWs &ws, hipStream_t s);
+                        int ncols, const TreeWs &ws, hipStream_t s, int target = 256);
 
 // Stage-2 launchers (brd_stage2.hip).
 template <typename T>

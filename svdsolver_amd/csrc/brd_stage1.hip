@@ -715,14 +715,14 @@ hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
 
 template <typename T>
 hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, int ncols,
-                        const TreeWs &ws, hipStream_t s)
+                        const TreeWs &ws, hipStream_t s, int target)
 {
     if (ncols <= 0) return hipSuccess;
     LvArgs a = lv_args(t, level);
     const int groups = t.lv[level].groups;
     const int nslabs = (ncols + kASlab - 1) / kASlab;
-    // one resident workgroup per CU (LDS bound): aim for about one wave of workgroups
-    const int target = 256;
+    // one resident workgroup per CU (registers): aim for about one wave of
+    // `target` workgroups (fewer than the CUs leaves room for a concurrent factor)
     const int spw = std::max(1, (groups * nslabs + target - 1) / target);
     dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
     const T *V = (const T *)ws.V[level], *VT = (const T *)ws.VT[level], *Tm = (const T *)ws.T[level];
@@ -735,7 +735,7 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
 
 template hipError_t launch_factor<double>(bool, double *, long, const Tree &, int, const TreeWs &, hipStream_t);
 template hipError_t launch_factor<float>(bool, float *, long, const Tree &, int, const TreeWs &, hipStream_t);
-template hipError_t launch_apply<double>(bool, double *, long, const Tree &, int, int, const TreeWs &, hipStream_t);
-template hipError_t launch_apply<float>(bool, float *, long, const Tree &, int, int, const TreeWs &, hipStream_t);
+template hipError_t launch_apply<double>(bool, double *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int);
+template hipError_t launch_apply<float>(bool, float *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int);
 
 }  // namespace brd

@@ -1,0 +1,35 @@
+"""Stage-1 timing under the current environment (developer tool): ge2band on
+an N x N fp64 matrix resident on the GPU, median of a few runs, with an
+agreement check of the band's |diagonal| against the first variant (/tmp)."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import svdsolver_amd as S  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+tag = sys.argv[2] if len(sys.argv) > 2 else "run"
+b = 32
+g = torch.Generator(device="cuda").manual_seed(5)
+A0 = torch.rand(n, n, dtype=torch.float64, device="cuda", generator=g) * 5
+ts = []
+for it in range(4):
+    A = A0.clone()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    S.ge2band(A, b)
+    torch.cuda.synchronize()
+    ts.append((time.perf_counter() - t0) * 1e3)
+ref = "/tmp/s1time_ref.npy"
+dd = np.abs(torch.diagonal(A, 1).cpu().numpy())
+if not os.path.exists(ref):
+    np.save(ref, dd)
+    dev = 0.0
+else:
+    r = np.load(ref)
+    dev = float(np.linalg.norm(dd - r) / np.linalg.norm(r))
+print(f"{tag}: stage1 n={n} median {np.median(ts):.2f} ms (runs {', '.join(f'{t:.1f}' for t in ts)}) |diag1| dev vs first {dev:.2e}")

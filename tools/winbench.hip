@@ -12,20 +12,6 @@
 namespace brd {
 
 // ---------------- candidate window code ------------------------------------
-// 1/sqrt(q) and 1/u: hardware estimate + two Newton steps (full precision)
-__device__ __forceinline__ double rsq_nr(double q) {
-    double r = __builtin_amdgcn_rsq(q);
-    double h = 0.5 * q;
-    r = r * fma(-h * r, r, 1.5);
-    r = r * fma(-h * r, r, 1.5);
-    return r;
-}
-__device__ __forceinline__ double rcp_nr(double u) {
-    double y = __builtin_amdgcn_rcp(u);
-    y = fma(y, fma(-u, y, 1.0), y);
-    y = fma(y, fma(-u, y, 1.0), y);
-    return y;
-}
 // reflector of x applied to a (x[0] = the pivot): the norm and sigma = sum_{c>=1} a_c x_c
 // are accumulated together; alpha = 1/u1, tau = -s u1 / ||x||.
 template <int B>

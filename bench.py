@@ -97,6 +97,68 @@ def cpu_baseline(n: int, band: int) -> dict:
             "kind": kind, "sample": f"one {n}x{n} fp64 two-stage reduction, b={band}, {dt:.2f} s"}
 
 
+def pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
+    (tools/pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled
+    for gfx950's 64-B tally of 128-B requests, MI355X_MICROARCH.md 'HBM').  The
+    counters cannot be read inside this process, so the profile of the same
+    command is the source; None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.txt")))
+    if not files:
+        return None, None
+    tot, cnt = 0.0, 0
+    for line in open(files[-1]):
+        if line.startswith(kernel_prefix):
+            f = line.split()
+            try:
+                d, two_fetch, wr = int(f[-4]), float(f[-2]), float(f[-1])
+            except (ValueError, IndexError):
+                continue
+            tot += d * (two_fetch + wr) * 1024 * 1024
+            cnt += d
+    return (tot / cnt if cnt else None), os.path.relpath(files[-1], REPO)
+
+
+def apply_roofline(ap, dtype):
+    """Stage-1 trailing update (k_apply): per element of the trailing matrix one
+    read + one write against 4b flops -> 8 flop/B at b = 32 fp64, below the
+    MFMA ridge (78.6 TF / 8 TB/s = 9.8 flop/B): HBM-bound."""
+    ms, launches = ap["ms"], max(ap["launches"], 1)
+    gbs = ap["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    tf = ap["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    traffic, src = pmc_traffic("void brd::k_apply<" + ("double" if dtype == "f64" else "float"))
+    return {"kernel": "k_apply (stage-1 trailing update, MFMA)", "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "traffic": round(traffic) if traffic else None, "traffic_source": src,
+            "algorithmic_bytes_per_launch": round(ap["bytes"] / launches),
+            "achieved_tflops": round(tf, 3), "mfma_peak_tflops": PEAK_TFLOPS[dtype],
+            "mfma_frac": round(tf / PEAK_TFLOPS[dtype], 4),
+            "launches": ap["launches"], "avg_launch_us": round(ms * 1e3 / launches, 3),
+            "flops_per_launch": round(ap["flops"] / launches)}
+
+
+def stage2_roofline(sw, n, b, dtype, steps):
+    """Stage 2 (k_band2bd_bundle, one launch per step): every bundle of sweeps
+    streams the band rows below its first sweep in and out once (P = 3b
+    elements per row), so the algorithmic HBM bytes are 2 * P * sizeof(T) *
+    sum over bundles of the rows; the kernel is bound by its chain of
+    dependent windows (about 4 per sweep), not by HBM (Stage 2)."""
+    esz = 8 if dtype == "f64" else 4
+    S = 2 if dtype == "f64" else 5
+    P = 3 * b
+    rows = sum(n - i0 for i0 in range(0, n - 1, S))
+    byt = 2.0 * P * esz * rows
+    ms = sw["ms"] / max(steps, 1)
+    traffic, src = pmc_traffic("void brd::k_band2bd_bundle<" + ("double" if dtype == "f64" else "float"))
+    gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"kernel": "k_band2bd_bundle (stage-2 sweeps)", "bound": "latency (dependent window chain)",
+            "ms": round(ms, 3), "hbm_gbs_algorithmic": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+            "algorithmic_bytes_per_launch": round(byt), "traffic": round(traffic) if traffic else None,
+            "traffic_source": src, "windows": n * ((n // b) * 2),
+            "us_per_sweep": round(ms * 1e3 / max(n - 1, 1), 3)}
+
+
 def main():
     args = parse()
     import torch
@@ -197,8 +259,6 @@ def main():
     matrices = 1 if (world == 1 or dist_mode) else world   # matrices reduced per step, whole job
     value = matrices * args.steps * flops_per / elapsed / 1e9
     if rank == 0:
-        ach = ap["flops"] / (ap["ms"] * 1e-3) / 1e12 if ap["ms"] > 0 else 0.0
-        peak = PEAK_TFLOPS[args.dtype]
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -219,13 +279,8 @@ def main():
                                        if dist_mode else f"replicas{world}")},
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
-            "roofline": {"kernel": "k_apply (stage-1 trailing update, MFMA)", "bound": "mfma",
-                         "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(ach / peak, 4), "traffic": None,
-                         "launches": ap["launches"],
-                         "avg_launch_us": round(ap["ms"] * 1e3 / max(ap["launches"], 1), 3),
-                         "flops_per_launch": round(ap["flops"] / max(ap["launches"], 1)),
-                         "hbm_gbs_algorithmic": round(ap["bytes"] / (ap["ms"] * 1e-3) / 1e9, 1) if ap["ms"] else 0},
+            "roofline": apply_roofline(ap, args.dtype),
+            "stage2": stage2_roofline(sw, n, b, args.dtype, args.steps),
             "kernel_ms_per_step": {"s1_apply": round(ap["ms"] / args.steps, 3),
                                    "s1_factor": round(fa["ms"] / args.steps, 3),
                                    "s2_sweep": round(sw["ms"] / args.steps, 3)},

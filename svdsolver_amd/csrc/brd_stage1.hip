@@ -26,6 +26,7 @@
 #include "brd_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace brd {

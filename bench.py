@@ -145,7 +145,7 @@ def stage2_roofline(sw, n, b, dtype, steps):
     sum over bundles of the rows; the kernel is bound by its chain of
     dependent windows (about 4 per sweep), not by HBM (Stage 2)."""
     esz = 8 if dtype == "f64" else 4
-    S = 2 if dtype == "f64" else 5
+    S = 3 if dtype == "f64" else 5      # sweeps per bundle (brd_stage2.hip bundle_plan)
     P = 3 * b
     rows = sum(n - i0 for i0 in range(0, n - 1, S))
     byt = 2.0 * P * esz * rows

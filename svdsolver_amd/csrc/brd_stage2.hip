@@ -706,7 +706,7 @@ __device__ __forceinline__ void lds_rel(int *p, int v) {
 // wave pair), else 1.
 template <bool EXACT, int KB> constexpr int bundle_w() { return (KB > 0 && !EXACT) ? 2 : 1; }
 template <typename T, int W> constexpr int bundle_max_threads() {
-    return sizeof(T) == 8 ? (W == 2 ? 512 : 320) : (W == 2 ? 1024 : 512);
+    return sizeof(T) == 8 ? (W == 2 ? 512 : 448) : (W == 2 ? 1024 : 512);
 }
 constexpr int kWriteRows = 32;  // rows per writer batch (at most)
 constexpr int kFly = 48;        // loader: rows in flight (LDS-DMA), <= 63
@@ -802,7 +802,7 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
         if (threadIdx.x == 0) S2STAMP(beta, 0);
 #ifdef BRD_STAMPS
         unsigned long long s2a[4] = {0, 0, 0, 0};
-        bool s2e[5] = {false, false, false, false, false};
+        bool s2e[7] = {false, false, false, false, false, false, false};
 #endif
 
         if (wave < W * nsw) {
@@ -885,6 +885,8 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
                     lds_rel(&F->front[wave], it.next_top(t));
                     lds_rel(&F->prog[wave], t + 1);
                     S2EV(beta, 0, wave == W * nsw - 1 && it.next_top(t) > beta * S + 300);
+                    S2EV(beta, 5, wave == 0 && t == 0);            // lead: first task done
+                    S2EV(beta, 6, wave == 0 && t == it.ntask - 1);  // lead: sweep done
                     if (wave == 0 && t == 0) S2STAMP(beta, 1);
                 }
             }
@@ -921,13 +923,21 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
                 bool moved = false;
                 if (ra < lim) {
                     if (ra >= 1 && ra <= dma_hi) {
-                        const int stop = min(lim, dma_hi + 1);
-                        for (; ra < stop; ++ra) {
-                            if (dma_lane) dma16_sc1(src, dst);
-                            src += rstep;
-                            dst += row_bytes;
-                            if (dst == ring_end) dst = ring_lds;
+                        const int k = min(lim, dma_hi + 1) - ra;
+                        if (dma_lane) {   // exec set once for the batch; loop control is uniform
+                            const char *p = src;
+                            unsigned d = dst;
+                            for (int i = 0; i < k; ++i) {
+                                dma16_sc1(p, d);
+                                p += rstep;
+                                d += row_bytes;
+                                if (d == ring_end) d = ring_lds;
+                            }
                         }
+                        src += (long)k * rstep;
+                        dst += (unsigned)k * row_bytes;
+                        if (dst >= ring_end) dst -= ring_end - ring_lds;
+                        ra += k;
                         moved = true;
                     } else if (ra == rl) {   // edge row, once the DMAs before it have landed
                         load_edge_row<T>(A, lda, n, b, ra, (T *)((char *)ring + (dst - ring_lds)), row_q, lane);
@@ -1093,7 +1103,7 @@ __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
 // run 3(S-1) tasks (1.5(S-1) window pairs of b rows) ahead of the trailing one,
 // plus a 2b-row window, plus S rows of sweep shift; checked against the exact
 // geometry in tests/test_stage2_schedule.py.
-int ring_min_rows(int b, int S) { return ((3 * (S - 1) + 1) / 2) * b + 2 * b + S + 8; }
+int ring_min_rows(int b, int S) { return ((3 * (S - 1)) / 2 + 2) * b + S + 8; }
 
 template <typename T, bool EXACT>
 static size_t bundle_lds_bytes(int b, int S, int R) {
@@ -1107,15 +1117,20 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
     int smax = EXACT ? 2 : (bundle_max_threads<T, W>() / 64 - 3) / W;
     if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
-    // Prefer the most sweeps whose ring keeps 2b rows of slack beyond the
-    // minimum (the loader's run-ahead); else the most that fit at all.
-    for (int slack : {2 * b, 8}) {
+    // Prefer the most sweeps whose ring keeps 16 rows of slack beyond the
+    // minimum (the loader's run-ahead; more sweeps per bundle amortise the
+    // inter-bundle hand-off, which dominates -- measured at N = 8192 fp64:
+    // S = 2 106 ms, S = 3 95 ms, S = 4 95 ms); else the most that fit at all.
+    const bool forced = senv && atoi(senv) > 0;   // a requested S only needs to fit
+    for (int slack : {forced ? 8 : 16, 8}) {
         for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
             const int rmin = ring_min_rows(b, S) + slack;
             if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
                 // largest ring that fits, but no more than n rows
+                static const char *renv = getenv("BRD_S2_RING");   // tuning: cap on ring rows
+                const int rcap = renv && atoi(renv) > 0 ? std::max(rmin, atoi(renv)) : 1 << 30;
                 R = rmin;
-                while (R < n + 1 && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
+                while (R < n + 1 && R + 8 <= rcap && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
                 return true;
             }
         }

@@ -73,7 +73,7 @@ def test_windows_fit_kernel_limits():
 
 def ring_min_rows(b, S):
     """Mirror of brd_stage2.hip ring_min_rows()."""
-    return ((3 * (S - 1) + 1) // 2) * b + 2 * b + S + 8
+    return ((3 * (S - 1)) // 2 + 2) * b + S + 8
 
 
 def exact_ring_need(n, b, S):
@@ -94,6 +94,7 @@ def exact_ring_need(n, b, S):
     return worst
 
 
-@pytest.mark.parametrize("n,b,S", [(300, 32, 1), (300, 32, 2), (300, 32, 3), (300, 32, 7), (200, 4, 15), (120, 8, 5)])
+@pytest.mark.parametrize("n,b,S", [(300, 32, 1), (300, 32, 2), (300, 32, 3), (300, 32, 4), (300, 32, 7), (200, 4, 15),
+                                   (120, 8, 5), (400, 16, 6), (257, 32, 5), (150, 2, 9)])
 def test_ring_size_formula_is_sufficient(n, b, S):
     assert ring_min_rows(b, S) >= exact_ring_need(n, b, S)

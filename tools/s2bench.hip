@@ -53,6 +53,19 @@ int main(int argc, char **argv) {
         std::vector<unsigned long long> ev((size_t)4096 * 8);
         (void)brd::read_s2ev(ev.data(), ev.size());
         printf("hand-off of row beta*S+300 (us, from the trail's front passing it): writer-published poller-seen loader-loaded lead-uses  | next bundle's t0 lag\n");
+        printf("bundle lag (lead task 0 done, us) and lead us/task, averaged over ranges of beta:\n");
+        const int rngs[][2] = {{0, 10}, {10, 100}, {100, 500}, {500, 1000}, {1000, 2000}, {2000, 3000}, {3000, 4000}};
+        for (auto &rg : rngs) {
+            if (rg[1] >= nb) continue;
+            double lag = (double)(ev[(size_t)rg[1] * 8 + 5] - ev[(size_t)rg[0] * 8 + 5]) / 100.0 / (rg[1] - rg[0]);
+            double tau = 0; int cnt = 0;
+            for (int beta = rg[0]; beta < rg[1]; ++beta) {
+                const int i = beta * S;
+                const int nt = 2 + 2 * ((n - std::min(i + 65, n)) / 32 + 1);
+                tau += (double)(ev[(size_t)beta * 8 + 6] - ev[(size_t)beta * 8 + 5]) / 100.0 / nt; ++cnt;
+            }
+            printf("  beta %4d..%4d: lag %.2f us/bundle, lead %.3f us/task\n", rg[0], rg[1], lag, tau / cnt);
+        }
         for (int beta : {1, 2, 3, 10, 100, 500, 1000, 2000, 3000}) {
             if (beta + 1 >= nb) continue;
             const unsigned long long *e0 = &ev[(size_t)beta * 8], *e1 = &ev[(size_t)(beta + 1) * 8];

@@ -709,6 +709,7 @@ template <typename T, int W> constexpr int bundle_max_threads() {
     return sizeof(T) == 8 ? (W == 2 ? 512 : 448) : (W == 2 ? 1024 : 512);
 }
 constexpr int kWriteRows = 32;  // rows per writer batch (at most)
+constexpr int kSubRows = 8;     // rows per writer sub-chunk (registers)
 constexpr int kFly = 48;        // loader: rows in flight (LDS-DMA), <= 63
 constexpr int kChunk = 8;       // loader: rows published per wait
 
@@ -1023,29 +1024,48 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
                 unsigned long long c1 = S2CLK();
                 S2ACC(beta, 0, c0, c1);
                 const int k = wt - wb;
-                u32x4 v[kWriteRows];
-                {
-                    int sl = acc.slot(wb);
+                const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
+                // the batch moves in sub-chunks of kSubRows rows (registers: one
+                // sub-chunk); each sub-chunk's slots are freed once it is read
+                int sl = acc.slot(wb);
+                const char *g = (const char *)(A + (long)wb * lda + wb - (b - 1)) + 16 * lane;
+                const long gstep = (lda + 1) * (long)sizeof(T);
+                for (int c = 0; c < k; c += kSubRows) {
+                    const int kc = min(kSubRows, k - c);
+                    u32x4 v[kSubRows];
                     const u32x4 *srow = (const u32x4 *)(ring + sl * P) + (lane < row_q ? lane : 0);
                     const int wrap = R - sl;   // rows before the ring wraps
 #pragma unroll
-                    for (int rr = 0; rr < kWriteRows; ++rr) {
-                        if (rr < k) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
-                    }
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) lds_rel(&F->freed, wt);   // slots reusable once read
-                const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
-                if (interior) {
-                    if (lane < row_q) {
-                        const char *g = (const char *)(A + (long)wb * lda + wb - (b - 1)) + 16 * lane;
-                        const long gstep = (lda + 1) * (long)sizeof(T);
+                    for (int rr = 0; rr < kSubRows; ++rr)
+                        if (rr < kc) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) lds_rel(&F->freed, wb + c + kc);   // slots reusable once read
+                    sl = sl + kc >= R ? sl + kc - R : sl + kc;
+                    if (interior) {
+                        if (lane < row_q) {
 #pragma unroll
-                        for (int rr = 0; rr < kWriteRows; ++rr) {
-                            if (rr < k) st16_sc1((void *)g, v[rr]);
-                            g += gstep;
+                            for (int rr = 0; rr < kSubRows; ++rr) {
+                                if (rr < kc) st16_sc1((void *)g, v[rr]);
+                                g += gstep;
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int rr = 0; rr < kSubRows; ++rr) {
+                            const int r = wb + c + rr;
+                            if (rr < kc && lane < row_q) {
+                                T *ge = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
+                                const int cc0 = r - (b - 1) + lane * kEpp<T>;
+                                T e[kEpp<T>];
+                                __builtin_memcpy(e, &v[rr], 16);
+#pragma unroll
+                                for (int kk = 0; kk < kEpp<T>; ++kk)
+                                    if (cc0 + kk >= 0 && cc0 + kk < n) st_c(ge + kk, e[kk]);
+                            }
                         }
                     }
+                }
+                if (interior) {
                     if (pend >= 0) {   // everything older than this batch's k stores has drained
                         unsigned long long c2 = S2CLK();
                         S2ACC(beta, 2, c1, c2);
@@ -1058,19 +1078,6 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
                     }
                     pend = wt;
                 } else {
-#pragma unroll
-                    for (int rr = 0; rr < kWriteRows; ++rr) {
-                        const int r = wb + rr;
-                        if (rr < k && lane < row_q) {
-                            T *g = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
-                            const int cc0 = r - (b - 1) + lane * kEpp<T>;
-                            T e[kEpp<T>];
-                            __builtin_memcpy(e, &v[rr], 16);
-#pragma unroll
-                            for (int kk = 0; kk < kEpp<T>; ++kk)
-                                if (cc0 + kk >= 0 && cc0 + kk < n) st_c(g + kk, e[kk]);
-                        }
-                    }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) st_c(rows_done + beta, wt);
                     pend = -1;

@@ -25,7 +25,8 @@ from typing import Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbrd_hip.so")
+# BRD_LIB: another build of the same library (developer A/B runs)
+LIB_PATH = os.environ.get("BRD_LIB") or os.path.join(_HERE, "lib", "libbrd_hip.so")
 
 BRD_DEVICE_PTR = 0x1
 BRD_ASYNC = 0x2

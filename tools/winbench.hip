@@ -12,8 +12,9 @@
 namespace brd {
 
 // ---------------- candidate window code ------------------------------------
-// reflector of x applied to a (x[0] = the pivot): the norm and sigma = sum_{c>=1} a_c x_c
-// are accumulated together; alpha = 1/u1, tau = -s u1 / ||x||.
+// every load of the window is issued before any arithmetic (sched_barrier), the
+// norm and sigma = sum_{c>=1} a_c x_c accumulate together; alpha = 1/u1 and
+// 1/||x|| by rcp / rsq + Newton steps.
 template <int B>
 __device__ __forceinline__ void refl_apply_v1(double (&a)[B], const double (&x)[B]) {
     double q[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
@@ -38,8 +39,67 @@ __device__ __forceinline__ void refl_apply_v1(double (&a)[B], const double (&x)[
 #pragma unroll
     for (int c = 1; c < B; ++c) a[c] = fma(-tda, x[c], a[c]);
 }
+// norm first (x only), sigma while the reflector scalars are formed
+template <int B>
+__device__ __forceinline__ void refl_apply_v2(double (&a)[B], const double (&x)[B]) {
+    double q[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < B; ++c) q[c & 3] = fma(x[c], x[c], q[c & 3]);
+    const double qq = (q[0] + q[1]) + (q[2] + q[3]);
+    const double rn = rsq_nr(qq);
+#pragma unroll
+    for (int c = 1; c < B; ++c) sg[c & 3] = fma(a[c], x[c], sg[c & 3]);
+    const double sigma = (sg[0] + sg[1]) + (sg[2] + sg[3]);
+    const double nrm = qq * rn;
+    const double s = x[0] >= 0.0 ? -1.0 : 1.0;
+    const double u1 = fma(-s, nrm, x[0]);
+    const double alpha = rcp_nr(u1);
+    const double tau = -s * u1 * rn;
+    const double dot = fma(alpha, sigma, a[0]);
+    const double td = tau * dot;
+    a[0] -= td;
+    const double tda = td * alpha;
+#pragma unroll
+    for (int c = 1; c < B; ++c) a[c] = fma(-tda, x[c], a[c]);
+}
 
 __device__ unsigned long long g_ph[8];
+template <int B, int RV>
+__device__ __forceinline__ void right_v1(const RingAcc<double> &A, int i1, int j1, int lane) {
+    const double *px = A.row(i1) + j1;
+    double *pa = A.row(i1 + lane) + j1;   // 2B = 64 rows: every lane
+    double a[B], x[B];
+#pragma unroll
+    for (int c = 0; c < B; ++c) x[c] = px[c];
+#pragma unroll
+    for (int c = 0; c < B; ++c) a[c] = pa[c];
+    __builtin_amdgcn_sched_barrier(0);
+    if (RV == 1) refl_apply_v1<B>(a, x); else refl_apply_v2<B>(a, x);
+#pragma unroll
+    for (int c = 0; c < B; ++c) pa[c] = a[c];
+}
+// left window: rows [i1, i1+B) x cols [j1, j1+2B), lane = column; rows that do
+// not wrap the ring sit (P-1) elements apart: one base address + immediate offsets
+template <int B, int P, int RV>
+__device__ __forceinline__ void left_v1(const RingAcc<double> &A, int i1, int j1, int lane) {
+    const int s0 = A.slot(i1);
+    double a[B], x[B];
+    if (s0 + B <= A.R) {
+        const double *bx = A.d + s0 * P + A.off - i1 + j1;
+        double *ba = const_cast<double *>(bx) + lane;
+#pragma unroll
+        for (int r = 0; r < B; ++r) x[r] = bx[r * (P - 1)];
+#pragma unroll
+        for (int r = 0; r < B; ++r) a[r] = ba[r * (P - 1)];
+        __builtin_amdgcn_sched_barrier(0);
+        if (RV == 1) refl_apply_v1<B>(a, x); else refl_apply_v2<B>(a, x);
+#pragma unroll
+        for (int r = 0; r < B; ++r) ba[r * (P - 1)] = a[r];
+    } else {
+        win_left_full<double, B>(A, i1, j1, lane);
+    }
+}
+
 template <typename T, int V, int B>
 __device__ __forceinline__ void win_right_v(const RingAcc<T> &A, int i1, int j1, int lane) {
     if constexpr (V == 0) {
@@ -49,33 +109,45 @@ __device__ __forceinline__ void win_right_v(const RingAcc<T> &A, int i1, int j1,
         const T *px = A.row(i1) + j1;
         T *pa = A.row(r) + j1;
         T a[B], x[B];
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         refl_apply_v1<B>(a, x);
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         if (lane < 2 * B) {
 #pragma unroll
             for (int c = 0; c < B; ++c) pa[c] = a[c];
         }
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         if (lane == 0) { g_ph[0] += t1 - t0; g_ph[1] += t2 - t1; g_ph[2] += t3 - t2; g_ph[3] += 1; }
-    } else {
-        const int r = i1 + (lane < 2 * B ? lane : 0);
-        const T *px = A.row(i1) + j1;
-        T *pa = A.row(r) + j1;
-        T a[B], x[B];
+    } else if constexpr (V == 4) {
+        double *pa = A.row(i1 + lane) + j1;
+        double a[B], x[B];
 #pragma unroll
-        for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
+        for (int c = 0; c < B; ++c) a[c] = pa[c];
+#pragma unroll
+        for (int c = 0; c < B; ++c)
+            x[c] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(a[c])),
+                                    __builtin_amdgcn_readfirstlane(__double2loint(a[c])));
         refl_apply_v1<B>(a, x);
-        if (lane < 2 * B) {
 #pragma unroll
-            for (int c = 0; c < B; ++c) pa[c] = a[c];
-        }
+        for (int c = 0; c < B; ++c) pa[c] = a[c];
+    } else if constexpr (V == 1) {
+        right_v1<B, 1>(A, i1, j1, lane);
+    } else {
+        right_v1<B, 2>(A, i1, j1, lane);
     }
 }
 template <typename T, int V, int B>
@@ -87,7 +159,9 @@ __device__ __forceinline__ void win_left_v(const RingAcc<T> &A, int i1, int j1, 
         int slot = A.slot(i1);
         T a[B], x[B];
         T *rows[B];
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < B; ++r) {
             rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
@@ -96,34 +170,45 @@ __device__ __forceinline__ void win_left_v(const RingAcc<T> &A, int i1, int j1, 
             slot = slot + 1 == A.R ? 0 : slot + 1;
         }
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         refl_apply_v1<B>(a, x);
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         if (lane < 2 * B) {
 #pragma unroll
             for (int r = 0; r < B; ++r) rows[r][col] = a[r];
         }
         __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         if (lane == 0) { g_ph[4] += t1 - t0; g_ph[5] += t2 - t1; g_ph[6] += t3 - t2; g_ph[7] += 1; }
+    } else if constexpr (V == 4) {
+        const int s0 = A.slot(i1);
+        constexpr int P = 96;
+        double a[B], x[B];
+        if (s0 + B <= A.R) {
+            double *ba = A.d + s0 * P + A.off - i1 + j1 + lane;
+#pragma unroll
+            for (int r = 0; r < B; ++r) a[r] = ba[r * (P - 1)];
+#pragma unroll
+            for (int r = 0; r < B; ++r)
+                x[r] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(a[r])),
+                                        __builtin_amdgcn_readfirstlane(__double2loint(a[r])));
+            refl_apply_v1<B>(a, x);
+#pragma unroll
+            for (int r = 0; r < B; ++r) ba[r * (P - 1)] = a[r];
+        } else {
+            win_left_full<double, B>(A, i1, j1, lane);
+        }
+    } else if constexpr (V == 1) {
+        left_v1<B, 96, 1>(A, i1, j1, lane);
     } else {
-        const int col = lane < 2 * B ? lane : 0;
-        int slot = A.slot(i1);
-        T a[B], x[B];
-        T *rows[B];
-#pragma unroll
-        for (int r = 0; r < B; ++r) {
-            rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
-            x[r] = rows[r][0];
-            a[r] = rows[r][col];
-            slot = slot + 1 == A.R ? 0 : slot + 1;
-        }
-        refl_apply_v1<B>(a, x);
-        if (lane < 2 * B) {
-#pragma unroll
-            for (int r = 0; r < B; ++r) rows[r][col] = a[r];
-        }
+        left_v1<B, 96, 2>(A, i1, j1, lane);
     }
 }
 
@@ -149,7 +234,9 @@ __global__ void __launch_bounds__(64) k_winbench(T *band, int n, int nsweeps, un
             const int wr = w.i2 - w.i1, wc = w.j2 - w.j1;
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_wave_barrier();
-            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
             if (right && wr == 2 * B && wc == B) {
                 win_right_v<T, V, B>(acc, w.i1, w.j1, lane);
             } else if (!right && wr == B && wc == 2 * B) {
@@ -164,7 +251,9 @@ __global__ void __launch_bounds__(64) k_winbench(T *band, int n, int nsweeps, un
             }
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_wave_barrier();
-            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
             if (right) { cr += t1 - t0; ++nr; } else { cl += t1 - t0; ++nl; }
         }
     }
@@ -205,16 +294,28 @@ int main() {
             s = s * 6364136223846793005ull + 1442695040888963407ull;
             h[(size_t)r * P + c - r + b - 1] = 1.0 + (double)(s >> 11) / 9007199254740992.0 * 4.0;
         }
-    std::vector<double> r0, r1, r2;
+    std::vector<double> r0, r1, r2, r3;
     run<0>(h, n, nsw, r0);
     run<1>(h, n, nsw, r1);
     run<2>(h, n, nsw, r2);
+    run<3>(h, n, nsw, r3);
+    std::vector<double> r4;
+    run<4>(h, n, nsw, r4);
     unsigned long long ph[8];
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(brd::g_ph), sizeof(ph));
     printf("phases right: load %.0f compute %.0f store %.0f | left: load %.0f compute %.0f store %.0f\n",
            (double)ph[0] / ph[3], (double)ph[1] / ph[3], (double)ph[2] / ph[3], (double)ph[4] / ph[7], (double)ph[5] / ph[7], (double)ph[6] / ph[7]);
     double md = 0, mx = 0;
-    for (size_t i = 0; i < r0.size(); ++i) { md = std::max(md, std::fabs(r0[i] - r1[i])); mx = std::max(mx, std::fabs(r0[i])); }
+    double md3 = 0;
+    for (size_t i = 0; i < r0.size(); ++i) {
+        md = std::max(md, std::fabs(r0[i] - r1[i]));
+        md3 = std::max(md3, std::fabs(r0[i] - r3[i]));
+        mx = std::max(mx, std::fabs(r0[i]));
+    }
+    printf("max |v0 - v3| = %.3e\n", md3);
+    md3 = 0;
+    for (size_t i = 0; i < r0.size(); ++i) md3 = std::max(md3, std::fabs(r0[i] - r4[i]));
+    printf("max |v0 - v4| = %.3e\n", md3);
     printf("max |v0 - v1| = %.3e (max |v0| = %.3e)\n", md, mx);
     return 0;
 }

@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--band", type=int, default=32)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-n", type=int, default=1024)
+    p.add_argument("--s2", choices=["compat", "sigma"], default="compat",
+                   help="stage-2 geometry: the reference's windows (the headline config) or the "
+                        "sigma-preserving variant (BRD_SIGMA)")
     p.add_argument("--mode", choices=["dist", "replicas"], default="dist",
                    help="N > 1: sharded stage 1 of one matrix (dist) or independent replicas")
     p.add_argument("--force-dist", action="store_true",
@@ -199,7 +202,7 @@ def main():
 
         def stage2(A):
             if rank == 0:
-                S.band2bd(Bfull, b, sync=False, extract=False)
+                S.band2bd(Bfull, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     else:
         base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
         mats = [base.clone() for _ in range(nmat)]
@@ -208,7 +211,7 @@ def main():
             S.ge2band(A, b, sync=False)
 
         def stage2(A):
-            S.band2bd(A, b, sync=False, extract=False)
+            S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
 
     for i in range(args.warmup):
@@ -273,7 +276,8 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic uniform [0,5) N x N, resident in HBM",
             "config": {"workload": f"two-stage bidiagonal reduction {n}x{n} {args.dtype}, band {b}, "
-                                   f"stage 2 = reference window geometry (compat)",
+                                   + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
+                                      else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
                        "n": n, "band": b, "global_batch": matrices,
                        "parallelism": (f"stage1 block-cyclic columns over {world} GPUs (RCCL), stage2 rank 0"
                                        if dist_mode else f"replicas{world}")},

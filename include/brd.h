@@ -47,6 +47,11 @@ enum brd_status {
                                  operation order (bit-identical to the reference's
                                  CPU code; slow, for verification)                 */
 #define BRD_NO_EXTRACT 0x8u   /* stage 2: do not write d/e (may pass NULL)         */
+#define BRD_SIGMA      0x10u  /* stage 2: sigma-preserving geometry -- the reference's
+                                 windows plus the final window pair each sweep
+                                 needs, so the result is orthogonally equivalent
+                                 to the band (not in the reference; combines
+                                 with BRD_EXACT_ORDER)                            */
 
 /* Stage 1: dense m x n (m >= n) -> upper band, bandwidth b (1 <= b <= 32).
  * On return A holds the band matrix: entries (i,j) with 0 <= j-i <= b, and
@@ -55,8 +60,9 @@ int brd_ge2band_f64(double *A, int m, int n, int lda, int b, int ngpus, unsigned
 int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned flags);
 
 /* Stage 2: n x n band (bandwidth b) -> bidiagonal, in place, with the
- * reference's window geometry (BRD_COMPAT).  d (n) and e (n-1) receive the
- * diagonal and super-diagonal (same memory kind as A). */
+ * reference's window geometry (BRD_COMPAT) or the sigma-preserving one
+ * (BRD_SIGMA).  d (n) and e (n-1) receive the diagonal and super-diagonal
+ * (same memory kind as A). */
 int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags);
 int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags);
 

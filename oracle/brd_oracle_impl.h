@@ -463,8 +463,17 @@ static int o_imin(int a, int b) { return a < b ? a : b; }
 /* Restates parallel::brd_p2 (svd_parallel.h:640-695): A is m x n row-major,
  * band width b (b super-diagonals).  In place; d (n) and e (n-1) receive the
  * diagonal and super-diagonal.  Returns 0, or -2 where the reference would
- * index an empty slice. */
-int OFN(oracle_brd_p2)(OT *A, int m, int n, int lda, int b, OT *d, OT *e)
+ * index an empty slice.
+ *
+ * sigma = 1: the sigma-preserving variant (not in the reference; SURVEY 8(f)
+ * rank 1).  The reference's window count nbtx = floor((n - j2) / (b' - 1))
+ * stops one window pair short of the matrix edge on most sweeps, so the last
+ * bulge is dropped and the result is not orthogonally equivalent to the band.
+ * With one more (clipped) pair per sweep, and empty windows skipped instead
+ * of failing, every reflector's fill is chased off the matrix and the
+ * bidiagonal has the band's singular values (tests/test_oracle.py checks
+ * this against numpy's SVD). */
+int OFN(oracle_brd_p2x)(OT *A, int m, int n, int lda, int b, OT *d, OT *e, int sigma)
 {
     if (b < 1 || m < 1 || n < 2 || lda < n)
         return -1;
@@ -485,18 +494,18 @@ int OFN(oracle_brd_p2)(OT *A, int m, int n, int lda, int b, OT *d, OT *e)
         rc = OFN(o_win_left)(A, lda, li1, li2, lj1, lj2, x, w, H, tmp);
         if (rc) break;
         /* nbtx = size_t(ceil((n - j2) / (b_size - 1))): integer division first (:664) */
-        int nbtx = (n - lj2) / (bs - 1);
+        int nbtx = (n - lj2) / (bs - 1) + (sigma ? 1 : 0);
         for (int k = 0; k < nbtx + 1; ++k) {
             int end_i = o_imin(li2 + bs - 1, m);
             int start_j = o_imin(lj1 + bs - 1, n);
             int end_j3 = o_imin(lj2 + bs - 1, n);
             int ri1 = li1, ri2 = end_i, rj1 = start_j, rj2 = lj2;
             li1 = li2; li2 = end_i; lj1 = start_j; lj2 = end_j3;
-            if (rj2 > rj1) {                   /* Task 2 */
+            if (rj2 > rj1 && (!sigma || ri2 > ri1)) {   /* Task 2 */
                 rc = OFN(o_win_right)(A, lda, ri1, ri2, rj1, rj2, x, w, H, tmp);
                 if (rc) break;
             }
-            if (lj2 > lj1) {                   /* Task 3 */
+            if (lj2 > lj1 && (!sigma || li2 > li1)) {   /* Task 3 */
                 rc = OFN(o_win_left)(A, lda, li1, li2, lj1, lj2, x, w, H, tmp);
                 if (rc) break;
             }
@@ -508,6 +517,11 @@ int OFN(oracle_brd_p2)(OT *A, int m, int n, int lda, int b, OT *d, OT *e)
     }
     free(x); free(w); free(H); free(tmp);
     return rc;
+}
+
+int OFN(oracle_brd_p2)(OT *A, int m, int n, int lda, int b, OT *d, OT *e)
+{
+    return OFN(oracle_brd_p2x)(A, m, n, lda, b, d, e, 0);
 }
 
 #undef OFN

@@ -41,6 +41,10 @@ def lib() -> ctypes.CDLL:
             g.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
             g.restype = ctypes.c_int
+            g = getattr(L, f"oracle_brd_p2x_{sfx}")
+            g.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+            g.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -64,17 +68,19 @@ def brd_p1(A: np.ndarray, t: int) -> np.ndarray:
     return A
 
 
-def brd_p2(A: np.ndarray, b: int):
+def brd_p2(A: np.ndarray, b: int, sigma: bool = False):
     """Band -> bidiagonal, reference windowed sweep (svd_parallel.h:640).
 
     Returns (A_out, d, e) where A_out is the full matrix after the sweeps
-    (what the reference writes to bidiagonal_*.bin)."""
+    (what the reference writes to bidiagonal_*.bin).  sigma=True: the
+    sigma-preserving variant (one more window pair per sweep; not in the
+    reference, see brd_oracle_impl.h)."""
     A = np.ascontiguousarray(A).copy()
     m, n = A.shape
     d = np.zeros(n, dtype=A.dtype)
     e = np.zeros(max(n - 1, 0), dtype=A.dtype)
-    rc = getattr(lib(), f"oracle_brd_p2_{_sfx(A)}")(A.ctypes.data, m, n, n, int(b),
-                                                     d.ctypes.data, e.ctypes.data)
+    rc = getattr(lib(), f"oracle_brd_p2x_{_sfx(A)}")(A.ctypes.data, m, n, n, int(b),
+                                                      d.ctypes.data, e.ctypes.data, int(bool(sigma)))
     if rc != 0:
         raise ValueError(f"oracle_brd_p2 failed rc={rc}")
     return A, d, e

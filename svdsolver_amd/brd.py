@@ -33,6 +33,7 @@ BRD_ASYNC = 0x2
 BRD_COMPAT = 0x0
 BRD_EXACT_ORDER = 0x4
 BRD_NO_EXTRACT = 0x8
+BRD_SIGMA = 0x10
 
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
@@ -168,14 +169,18 @@ cuda_brd_p1 = brd_p1   # name of the reference GPU entry point (svd_cuda_2.cu:11
 # ---------------------------------------------------------------------------
 # stage 2
 # ---------------------------------------------------------------------------
-def band2bd(A, b: int, *, exact_order: bool = False, sync: bool = True, extract: bool = True):
-    """Band -> bidiagonal IN PLACE with the reference's window geometry.
+def band2bd(A, b: int, *, exact_order: bool = False, sigma: bool = False, sync: bool = True,
+            extract: bool = True):
+    """Band -> bidiagonal IN PLACE with the reference's window geometry, or
+    (``sigma``) the sigma-preserving one: the bidiagonal then has the band's
+    singular values (BRD_SIGMA, include/brd.h).
     Returns (d, e) (None, None when ``extract`` is False)."""
     m, n = A.shape
     assert m == n, "stage 2 takes a square band matrix"
     sfx = _sfx(A.dtype)
     fn = f"brd_band2bd_{sfx}"
-    flags = (BRD_EXACT_ORDER if exact_order else 0) | (0 if extract else BRD_NO_EXTRACT)
+    flags = ((BRD_EXACT_ORDER if exact_order else 0) | (BRD_SIGMA if sigma else 0)
+             | (0 if extract else BRD_NO_EXTRACT))
     if _is_torch_cuda(A):
         import torch
         _bind_stream(A)
@@ -195,11 +200,12 @@ def band2bd(A, b: int, *, exact_order: bool = False, sync: bool = True, extract:
     return (d, e[: n - 1]) if extract else (None, None)
 
 
-def brd_p2(A, b: int, *, exact_order: bool = False) -> Tuple[object, object, object]:
+def brd_p2(A, b: int, *, exact_order: bool = False, sigma: bool = False) -> Tuple[object, object, object]:
     """Reference-compatible band -> bidiagonal: returns (A_after, d, e), where
-    A_after is what the reference writes to bidiagonal_*.bin."""
+    A_after is what the reference writes to bidiagonal_*.bin (``sigma``: the
+    sigma-preserving variant, not in the reference)."""
     B = A.contiguous().clone() if _is_torch_cuda(A) else np.array(A, copy=True, order="C")
-    d, e = band2bd(B, b, exact_order=exact_order)
+    d, e = band2bd(B, b, exact_order=exact_order, sigma=sigma)
     return B, d, e
 
 

@@ -220,13 +220,13 @@ static void prof_drain() {
 // Runs the stage-2 sweep on a device matrix; checks the kernel's spin-limit
 // word when the call is synchronous.
 template <typename T>
-static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sync, hipStream_t s) {
+static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sigma, bool sync, hipStream_t s) {
     int rc = ensure_s2_flags(n);
     if (rc) return rc;
     int *prog = g_ctx.s2_flags, *err = g_ctx.s2_flags + n + 1;
     {
         ProfScope ps("s2_sweep", 0, 0, s);
-        HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, prog, err, s2_waves(), s));
+        HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, sigma, prog, err, s2_waves(), s));
     }
     if (sync) {
         HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -396,11 +396,12 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
     const bool extract = !(flags & BRD_NO_EXTRACT);
     if (extract && (!dd || !ee)) return fail(BRD_EINVAL, "d/e are NULL (pass BRD_NO_EXTRACT to skip them)");
     const bool exact = (flags & BRD_EXACT_ORDER) != 0;
+    const bool sigma = (flags & BRD_SIGMA) != 0;
     hipStream_t s = stream();
     const bool dev = (flags & BRD_DEVICE_PTR) != 0;
     if (dev) {
         if (!is_device_ptr(A)) return fail(BRD_EINVAL, "BRD_DEVICE_PTR set but A is not device memory");
-        int rc = band2bd_device<T>(A, n, lda, b, exact, !(flags & BRD_ASYNC), s);
+        int rc = band2bd_device<T>(A, n, lda, b, exact, sigma, !(flags & BRD_ASYNC), s);
         if (rc) return rc;
         if (extract) HIP_TRY(launch_extract_bidiag<T>(A, n, lda, dd, ee, s));
         if (!(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
@@ -411,7 +412,7 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
         de = d + (size_t)n * n;
         HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, n,
                                  hipMemcpyHostToDevice, s));
-        int rc = band2bd_device<T>(d, n, n, b, exact, true, s);
+        int rc = band2bd_device<T>(d, n, n, b, exact, sigma, true, s);
         if (rc) { hipFree(d); return rc; }
         HIP_TRY(launch_extract_bidiag<T>(d, n, n, de, de + n, s));
         HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, n,

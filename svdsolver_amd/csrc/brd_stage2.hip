@@ -568,10 +568,13 @@ struct SweepIter {
     int i;              // sweep index
     int ntask;          // 2 + 2*(nbtx+1)
     Win tl;             // running t_left
-    __device__ void init(int m_, int n_, int b, int i_) {
+    // sigma = 1: the sigma-preserving geometry (BRD_SIGMA): one more window
+    // pair per sweep, so the last bulge is chased off the matrix instead of
+    // dropped (oracle_brd_p2x; empty windows are skipped by the callers)
+    __device__ void init(int m_, int n_, int b, int i_, int sigma) {
         m = m_; n = n_; bs = b + 1; i = i_;
         const int tl_j2 = min(i + bs + bs - 1, n);
-        const int nbtx = (n - tl_j2) / (bs - 1);
+        const int nbtx = (n - tl_j2) / (bs - 1) + sigma;
         ntask = 2 + 2 * (nbtx + 1);
     }
     // Window of task t (tasks must be requested in order 0,1,2,...).
@@ -608,9 +611,9 @@ struct SweepIter {
 
 constexpr int kSpinLimit = 1 << 24;
 
-__device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i) {
+__device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i, int sigma) {
     SweepIter it;
-    it.init(m, n, b, i);
+    it.init(m, n, b, i, sigma);
     return it.ntask;
 }
 
@@ -626,7 +629,7 @@ __device__ __forceinline__ int sweep_ntask(int m, int n, int b, int i) {
 // wave polls that flag with sc1 loads before its own sc1 loads.
 // ==========================================================================
 template <typename T, bool EXACT>
-__global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long lda, int b, int *prog,
+__global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long lda, int b, int sigma, int *prog,
                                                      int *err)
 {
     __shared__ WaveLds<T, EXACT> S;
@@ -635,8 +638,8 @@ __global__ void __launch_bounds__(64) k_band2bd_pipe(T *A, int m, int n, long ld
     const HbmAcc<T> acc{A, lda};
     for (int i = blockIdx.x; i < n - 1; i += nw) {
         SweepIter it;
-        it.init(m, n, b, i);
-        const int prev_ntask = i > 0 ? sweep_ntask(m, n, b, i - 1) : 0;
+        it.init(m, n, b, i, sigma);
+        const int prev_ntask = i > 0 ? sweep_ntask(m, n, b, i - 1, sigma) : 0;
         for (int t = 0; t < it.ntask; ++t) {
             bool right;
             const Win wnd = it.task(t, right);
@@ -777,7 +780,7 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
 
 template <typename T, bool EXACT, int KB, int W>
 __global__ void __launch_bounds__((bundle_max_threads<T, W>()))
-k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int *rows_done, int *err)
+k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int P = ring_pitch<T>(b);
@@ -816,8 +819,8 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int S, int R, unsigned magic, int
             const int sw = wave / W, pw = wave - sw * W;
             const int i = i0 + sw;
             SweepIter it;
-            it.init(n, n, b, i);
-            const int prev_ntask = sw > 0 ? sweep_ntask(n, n, b, i - 1) : 0;
+            it.init(n, n, b, i, sigma);
+            const int prev_ntask = sw > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
             for (int t = 0; t < it.ntask; ++t) {
                 bool right;
                 const Win wnd = it.task(t, right);
@@ -1147,13 +1150,14 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
 
 // prog: n+1 ints, err: 1 int (device workspace, zeroed here).
 template <typename T>
-hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *prog, int *err,
+hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,
                           int nwaves, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(prog, 0, sizeof(int) * (size_t)(n + 1), s);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
+    const int sg = sigma_geom ? 1 : 0;
     static const char *sel = getenv("BRD_S2_SCHEDULE");   // "pipe" selects the HBM-only schedule
     const bool pipe = sel && sel[0] == 'p';
     int S = 0, R = 0;
@@ -1176,20 +1180,20 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, int *p
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 2)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (fast32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const int grid = std::max(1, std::min(nwaves, n - 1));
     if (exact_order)
-        hipLaunchKernelGGL((k_band2bd_pipe<T, true>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, prog, err);
+        hipLaunchKernelGGL((k_band2bd_pipe<T, true>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, sg, prog, err);
     else
-        hipLaunchKernelGGL((k_band2bd_pipe<T, false>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, prog, err);
+        hipLaunchKernelGGL((k_band2bd_pipe<T, false>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, sg, prog, err);
     return hipGetLastError();
 }
 
@@ -1200,8 +1204,8 @@ hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStr
     return hipGetLastError();
 }
 
-template hipError_t launch_band2bd<double>(double *, int, long, int, bool, int *, int *, int, hipStream_t);
-template hipError_t launch_band2bd<float>(float *, int, long, int, bool, int *, int *, int, hipStream_t);
+template hipError_t launch_band2bd<double>(double *, int, long, int, bool, bool, int *, int *, int, hipStream_t);
+template hipError_t launch_band2bd<float>(float *, int, long, int, bool, bool, int *, int *, int, hipStream_t);
 template hipError_t launch_extract_bidiag<double>(const double *, int, long, double *, double *, hipStream_t);
 template hipError_t launch_extract_bidiag<float>(const float *, int, long, float *, float *, hipStream_t);
 

@@ -198,3 +198,63 @@ def test_stage2_fast_vs_exact_order_3000_b32(S):
     _, d_f, e_f = S.brd_p2(band, b)
     err = _bd_err(d_f, e_f, d_x, e_x)
     assert err <= 10 * env + 1e-14, (err, env)
+
+
+# ---- sigma-preserving stage 2 (BRD_SIGMA) --------------
+# Not in the reference: its window count stops one window pair short of the
+# matrix edge on most sweeps (oracle/brd_oracle_impl.h, oracle_brd_p2x), so
+# its bidiagonal is not orthogonally equivalent to the band.  With the extra
+# pair the reduction is orthogonal: the bidiagonal's singular values are the
+# band's (and, after stage 1, the input matrix's) to rounding.
+def _sv_bidiag(d, e):
+    n = len(d)
+    B = np.zeros((n, n))
+    B[np.arange(n), np.arange(n)] = np.asarray(d, dtype=np.float64)
+    B[np.arange(n - 1), np.arange(1, n)] = np.asarray(e, dtype=np.float64)
+    return np.linalg.svd(B, compute_uv=False)
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
+@pytest.mark.parametrize("b", [4, 32])
+def test_stage2_sigma_exact_order_bit_identical_to_oracle(S, T, b):
+    """exact-order + sigma: the oracle's arithmetic, bit for bit (n = 512)."""
+    from oracle import oracle
+    A = G.ref_bin(f"test_{T}_512_512.bin", 512, T)
+    band = oracle.brd_p1(A, b)
+    ref, d_o, e_o = oracle.brd_p2(band, b, sigma=True)
+    out, d, e = S.brd_p2(band, b, exact_order=True, sigma=True)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(d, d_o) and np.array_equal(e, e_o)
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
+@pytest.mark.parametrize("b", [4, 32])
+def test_stage2_sigma_fast_vs_oracle(S, T, b):
+    """fast arithmetic + sigma vs the oracle: the reduction is orthogonal (well
+    conditioned), so |d|, |e| agree to rounding -- no chaotic envelope here."""
+    from oracle import oracle
+    A = G.input1024(T)
+    band = oracle.brd_p1(A, b)
+    _, d_o, e_o = oracle.brd_p2(band, b, sigma=True)
+    _, d, e = S.brd_p2(band, b, sigma=True)
+    sv_o, sv = _sv_bidiag(d_o, e_o), _sv_bidiag(d, e)
+    tol = 1e-12 if T == "double" else 2e-5
+    assert np.max(np.abs(sv - sv_o)) / sv_o[0] < tol
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
+def test_two_stage_sigma_preserves_singular_values(S, T):
+    """GPU stage 1 + GPU sigma stage 2 at n = 2048, b = 32: the bidiagonal's
+    singular values are the dense input's (numpy SVD), fp64 to 1e-12 of
+    sigma_max; the compat geometry is 1e-2 .. 1e-1 off on the same input."""
+    rng = np.random.default_rng(21)
+    n, b = 2048, 32
+    dt = np.float64 if T == "double" else np.float32
+    A = rng.uniform(0, 5, (n, n)).astype(dt)
+    sv_ref = np.linalg.svd(A.astype(np.float64), compute_uv=False)
+    band = S.brd_p1(A, b)
+    _, d, e = S.brd_p2(band, b, sigma=True)
+    err = np.max(np.abs(_sv_bidiag(d, e) - sv_ref)) / sv_ref[0]
+    assert err < (1e-12 if T == "double" else 1e-5), err
+    _, dc, ec = S.brd_p2(band, b)
+    assert np.max(np.abs(_sv_bidiag(dc, ec) - sv_ref)) / sv_ref[0] > 100 * err

@@ -9,7 +9,7 @@ windows are enumerated exactly as the reference's brd_p2 builds them
 import pytest
 
 
-def windows(m, n, b):
+def windows(m, n, b, sigma=False):
     bs = b + 1
     W = {}
     for i in range(n - 1):
@@ -17,7 +17,7 @@ def windows(m, n, b):
         tasks = [tl]
         tl = (i + 1, min(i + bs, m), i + 1, min(i + 2 * bs - 1, n))
         tasks.append(tl)
-        nbtx = (n - tl[3]) // (bs - 1)
+        nbtx = (n - tl[3]) // (bs - 1) + (1 if sigma else 0)
         for _ in range(nbtx + 1):
             end_i = min(tl[1] + bs - 1, m)
             sj = min(tl[2] + bs - 1, n)
@@ -33,8 +33,8 @@ def _overlap(a, b):
     return a[0] < b[1] and b[0] < a[1] and a[2] < b[3] and b[2] < a[3]
 
 
-def worst_slack(n, b, lag):
-    W = windows(n, n, b)
+def worst_slack(n, b, lag, sigma=False):
+    W = windows(n, n, b, sigma)
     worst = -10 ** 9
     for i in W:
         for ip in range(i + 1, min(n - 1, i + 2 * b + 4)):
@@ -47,9 +47,10 @@ def worst_slack(n, b, lag):
     return worst
 
 
+@pytest.mark.parametrize("sigma", [False, True])
 @pytest.mark.parametrize("n,b", [(64, 4), (100, 4), (130, 8), (128, 32), (257, 32), (300, 16), (50, 2), (40, 1)])
-def test_lag3_preserves_serial_order(n, b):
-    assert worst_slack(n, b, 3) <= 0
+def test_lag3_preserves_serial_order(n, b, sigma):
+    assert worst_slack(n, b, 3, sigma) <= 0
 
 
 @pytest.mark.parametrize("n,b", [(64, 4), (128, 32)])
@@ -57,10 +58,11 @@ def test_lag2_is_not_enough(n, b):
     assert worst_slack(n, b, 2) > 0
 
 
-def test_windows_fit_kernel_limits():
+@pytest.mark.parametrize("sigma", [False, True])
+def test_windows_fit_kernel_limits(sigma):
     """Right windows <= 2b x b, left windows <= b x 2b (one row/column per lane)."""
     for n, b in [(257, 32), (100, 4), (64, 1)]:
-        for i, tasks in windows(n, n, b).items():
+        for i, tasks in windows(n, n, b, sigma).items():
             for t, w in enumerate(tasks):
                 if w is None:
                     continue
@@ -76,12 +78,12 @@ def ring_min_rows(b, S):
     return ((3 * (S - 1)) // 2 + 2) * b + S + 8
 
 
-def exact_ring_need(n, b, S):
+def exact_ring_need(n, b, S, sigma=False):
     """Rows the LDS ring must hold so the trailing sweep of a bundle can always
     progress: from the trailing sweep's next window top to the bottom of the
     leading sweep's window 3(S-1) tasks ahead (its predecessors' bottoms are
     at most S-1 rows lower)."""
-    W = windows(n, n, b)
+    W = windows(n, n, b, sigma)
     worst = 0
     for i0 in range(0, n - S):
         lead, trail = W[i0], W[i0 + S - 1]
@@ -98,3 +100,4 @@ def exact_ring_need(n, b, S):
                                    (120, 8, 5), (400, 16, 6), (257, 32, 5), (150, 2, 9)])
 def test_ring_size_formula_is_sufficient(n, b, S):
     assert ring_min_rows(b, S) >= exact_ring_need(n, b, S)
+    assert ring_min_rows(b, S) >= exact_ring_need(n, b, S, sigma=True)

@@ -23,7 +23,7 @@ int main(int argc, char **argv) {
         (void)hipMemcpy(A, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice);
         (void)brd::reset_s2tt();
         (void)hipEventRecord(e0);
-        (void)brd::launch_band2bd<double>(A, n, n, b, false, flags, flags + n + 1, 256, 0);
+        (void)brd::launch_band2bd<double>(A, n, n, b, false, getenv("BRD_SIGMA") != nullptr, flags, flags + n + 1, 256, 0);
         (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
         printf("stage2 n=%d: %.2f ms\n", n, ms);

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(64) k_winbench(T *band, int n, int nsweeps, un
     int nr = 0, nl = 0;
     for (int i = 0; i < nsweeps; ++i) {
         SweepIter it;
-        it.init(n, n, B, i);
+        it.init(n, n, B, i, 0);
         for (int t = 0; t < it.ntask; ++t) {
             bool right;
             const Win w = it.task(t, right);

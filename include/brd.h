@@ -66,6 +66,14 @@ int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned 
 int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags);
 int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags);
 
+/* Singular values of the upper bidiagonal (d (n), e (n-1)), host memory, in
+ * descending order into sv (n): Golub-Kahan QR with Wilkinson shifts, values
+ * only (replaces the reference's serial::qrd, svd_serial.h:368).  After
+ * brd_band2bd_* with BRD_SIGMA these are the singular values of the matrix
+ * stage 1 started from. */
+int brd_bdsvd_f64(const double *d, const double *e, int n, double *sv);
+int brd_bdsvd_f32(const float *d, const float *e, int n, float *sv);
+
 /* Stream used by subsequent calls (hipStream_t; NULL = the legacy default
  * stream).  Until the first call the library uses a stream of its own;
  * brd_use_own_stream() reverts to it. */

@@ -4,8 +4,8 @@
 The compute path is libbrd_hip.so (hand-written gfx950 HIP kernels behind the
 C ABI in include/brd.h); this package is its Python host side.
 """
-from .brd import (BRD_DEVICE_PTR, BRD_EXACT_ORDER, BRD_NO_EXTRACT, BrdError, LIB_PATH,  # noqa: F401
-                  band2bd, brd_p1, brd_p2, cuda_brd_p1, ge2band, lib, profile_enable,
-                  profile_query, profile_reset)
+from .brd import (BRD_DEVICE_PTR, BRD_EXACT_ORDER, BRD_NO_EXTRACT, BRD_SIGMA, BrdError, LIB_PATH,  # noqa: F401
+                  band2bd, bdsvd, brd_p1, brd_p2, cuda_brd_p1, ge2band, lib, profile_enable,
+                  profile_query, profile_reset, singular_values)
 
-__all__ = ["ge2band", "band2bd", "brd_p1", "brd_p2", "cuda_brd_p1", "BrdError"]
+__all__ = ["ge2band", "band2bd", "brd_p1", "brd_p2", "cuda_brd_p1", "bdsvd", "singular_values", "BrdError"]

@@ -40,7 +40,7 @@ EXPORTED = (
     "brd_set_stream", "brd_use_own_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
     "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
-    "brd_last_error", "brd_version",
+    "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_last_error", "brd_version",
 )
 
 # brd_coll_fn (include/brd.h): int (*)(int op, const void *send, void *recv,
@@ -71,6 +71,9 @@ def _load() -> ctypes.CDLL:
         g = getattr(L, f"brd_band2bd_{t}")
         g.argtypes = [vp, ci, ci, ci, vp, vp, cu]
         g.restype = ci
+        h = getattr(L, f"brd_bdsvd_{t}")
+        h.argtypes = [vp, vp, ci, vp]
+        h.restype = ci
     L.brd_set_stream.argtypes = [vp]
     L.brd_set_stream.restype = ci
     L.brd_use_own_stream.argtypes = []
@@ -207,6 +210,38 @@ def brd_p2(A, b: int, *, exact_order: bool = False, sigma: bool = False) -> Tupl
     B = A.contiguous().clone() if _is_torch_cuda(A) else np.array(A, copy=True, order="C")
     d, e = band2bd(B, b, exact_order=exact_order, sigma=sigma)
     return B, d, e
+
+
+# ---------------------------------------------------------------------------
+# bidiagonal -> singular values (host), and the whole pipeline
+# ---------------------------------------------------------------------------
+def bdsvd(d, e):
+    """Singular values (descending) of the upper bidiagonal (d, e) via the
+    library's host Golub-Kahan QR (brd_bdsvd_*; replaces the reference's
+    serial::qrd, svd_serial.h:368).  d, e: numpy arrays or torch tensors."""
+    if _is_torch_cuda(d):
+        d, e = d.cpu().numpy(), e.cpu().numpy()
+    d = np.ascontiguousarray(d)
+    e = np.ascontiguousarray(e, dtype=d.dtype)
+    n = d.shape[0]
+    if e.shape[0] != max(n - 1, 0):
+        raise ValueError("e must have n - 1 entries")
+    sfx = _sfx(d.dtype)
+    sv = np.empty(n, dtype=d.dtype)
+    ep = e if n > 1 else np.zeros(1, dtype=d.dtype)
+    fn = f"brd_bdsvd_{sfx}"
+    _check(fn, getattr(lib, fn)(ctypes.c_void_p(d.ctypes.data), ctypes.c_void_p(ep.ctypes.data), n,
+                                ctypes.c_void_p(sv.ctypes.data)))
+    return sv
+
+
+def singular_values(A, b: int = 32):
+    """Singular values of the square matrix A: stage 1 (dense -> band, GPU),
+    stage 2 with the sigma-preserving geometry (GPU), then bdsvd (host).
+    A is not modified."""
+    B = brd_p1(A, b)
+    _, d, e = brd_p2(B, b, sigma=True)
+    return bdsvd(d, e)
 
 
 # ---------------------------------------------------------------------------

@@ -258,3 +258,16 @@ def test_two_stage_sigma_preserves_singular_values(S, T):
     assert err < (1e-12 if T == "double" else 1e-5), err
     _, dc, ec = S.brd_p2(band, b)
     assert np.max(np.abs(_sv_bidiag(dc, ec) - sv_ref)) / sv_ref[0] > 100 * err
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
+def test_singular_values_pipeline(S, T):
+    """S.singular_values: GPU stage 1 + GPU sigma stage 2 + host bdsvd give the
+    singular values of a dense 1024 x 1024 input (numpy's SVD) to
+    1e-12 sigma_max (fp64) / 1e-5 (fp32)."""
+    rng = np.random.default_rng(31)
+    dt = np.float64 if T == "double" else np.float32
+    A = rng.uniform(0, 5, (1024, 1024)).astype(dt)
+    sv = S.singular_values(A, 32)
+    ref = np.linalg.svd(A.astype(np.float64), compute_uv=False)
+    assert np.max(np.abs(sv.astype(np.float64) - ref)) / ref[0] < (1e-12 if T == "double" else 1e-5)

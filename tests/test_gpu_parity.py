@@ -271,3 +271,18 @@ def test_singular_values_pipeline(S, T):
     sv = S.singular_values(A, 32)
     ref = np.linalg.svd(A.astype(np.float64), compute_uv=False)
     assert np.max(np.abs(sv.astype(np.float64) - ref)) / ref[0] < (1e-12 if T == "double" else 1e-5)
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
+def test_one_stage_band1_is_bidiagonal_with_input_singular_values(S, T):
+    """brd_ge2band with b = 1 is the one-stage reduction straight to bidiagonal
+    form (the comparison baseline, tools/onestage.py): exact zeros outside the
+    two diagonals and the input's singular values."""
+    rng = np.random.default_rng(41)
+    dt = np.float64 if T == "double" else np.float32
+    A = rng.uniform(0, 5, (384, 384)).astype(dt)
+    B = S.brd_p1(A, 1)
+    assert _outside_band_zero(B, 1)
+    sv = S.bdsvd(np.diagonal(B).copy(), np.diagonal(B, 1).copy())
+    ref = np.linalg.svd(A.astype(np.float64), compute_uv=False)
+    assert np.max(np.abs(sv.astype(np.float64) - ref)) / ref[0] < (1e-12 if T == "double" else 1e-5)

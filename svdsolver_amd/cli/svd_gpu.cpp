@@ -13,6 +13,12 @@
 //       N = k*step for k = 1..nsteps, ninst matrices uniform in [0,5) each;
 //       prints "N = <n> | <sec> sec" per size and writes the reference's 2-row
 //       CSV (N row, stage-1 seconds row) plus a third row with stage-2 seconds.
+//   svd_gpu svd <N> [--dtype f32|f64] [--band B]
+//       Singular values of an N x N matrix uniform in [0,5): stage 1, stage 2 with
+//       the sigma-preserving geometry (BRD_SIGMA) and the host bidiagonal QR
+//       (brd_bdsvd_*, the reference's serial::qrd step); prints the largest and
+//       smallest values and the time of each step (not in the reference CLI).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +38,16 @@ template <> int ge2band<float>(float *A, int n, int b) { return brd_ge2band_f32(
 template <typename T> int band2bd(T *A, int n, int b, T *d, T *e);
 template <> int band2bd<double>(double *A, int n, int b, double *d, double *e) { return brd_band2bd_f64(A, n, n, b, d, e, 0); }
 template <> int band2bd<float>(float *A, int n, int b, float *d, float *e) { return brd_band2bd_f32(A, n, n, b, d, e, 0); }
+template <typename T> int band2bd_sigma(T *A, int n, int b, T *d, T *e);
+template <> int band2bd_sigma<double>(double *A, int n, int b, double *d, double *e) {
+    return brd_band2bd_f64(A, n, n, b, d, e, BRD_SIGMA);
+}
+template <> int band2bd_sigma<float>(float *A, int n, int b, float *d, float *e) {
+    return brd_band2bd_f32(A, n, n, b, d, e, BRD_SIGMA);
+}
+template <typename T> int bdsvd(const T *d, const T *e, int n, T *sv);
+template <> int bdsvd<double>(const double *d, const double *e, int n, double *sv) { return brd_bdsvd_f64(d, e, n, sv); }
+template <> int bdsvd<float>(const float *d, const float *e, int n, float *sv) { return brd_bdsvd_f32(d, e, n, sv); }
 
 void die(const char *what, int rc) {
     std::fprintf(stderr, "%s failed (%d): %s\n", what, rc, brd_last_error());
@@ -109,6 +125,33 @@ int benchmark(int step, int nsteps, int ninst, int b, const std::string &csv) {
     return 0;
 }
 
+template <typename T>
+int svd(int n, int b) {
+    brd::Matrix<T> A(n, n);
+    A.fill(T(0), T(5), 1000003ull * n);
+    std::vector<T> d(n), e(n), sv(n);
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = ge2band<T>(A.data(), n, b);
+    if (rc) die("brd_ge2band", rc);
+    auto t1 = std::chrono::steady_clock::now();
+    rc = band2bd_sigma<T>(A.data(), n, b, d.data(), e.data());
+    if (rc) die("brd_band2bd (BRD_SIGMA)", rc);
+    auto t2 = std::chrono::steady_clock::now();
+    rc = bdsvd<T>(d.data(), e.data(), n, sv.data());
+    if (rc) die("brd_bdsvd", rc);
+    auto t3 = std::chrono::steady_clock::now();
+    auto sec = [](auto a, auto z) { return std::chrono::duration<double>(z - a).count(); };
+    std::printf("N = %d (%s, band %d): dense -> band %g sec | band -> bidiagonal %g sec | bidiagonal -> "
+                "values %g sec (host)\n", n, sizeof(T) == 8 ? "fp64" : "fp32", b, sec(t0, t1), sec(t1, t2), sec(t2, t3));
+    const int k = std::min(n, 5);
+    std::printf("largest :");
+    for (int i = 0; i < k; ++i) std::printf(" %.12g", (double)sv[i]);
+    std::printf("\nsmallest:");
+    for (int i = n - k; i < n; ++i) std::printf(" %.12g", (double)sv[i]);
+    std::printf("\n");
+    return 0;
+}
+
 void help() {
     std::printf("Options for MI355X two-stage bidiagonal reduction\n"
                 "\n(1) Run benchmark tests.\n"
@@ -117,7 +160,10 @@ void help() {
                 "\tExample: ./svd_gpu benchmark 1024 4 1 32\n"
                 "\n(2) Correctness test against the reference fixtures (band size 4).\n"
                 "\t>> check [64|512|1024] [--dtype f32|f64] [--data-dir DIR]\n"
-                "\tExample: ./svd_gpu check 64\n");
+                "\tExample: ./svd_gpu check 64\n"
+                "\n(3) Singular values (stage 1, sigma-preserving stage 2, host bidiagonal QR).\n"
+                "\t>> svd [<int> N] [--dtype f32|f64] [--band B]\n"
+                "\tExample: ./svd_gpu svd 2048 --dtype f64\n");
 }
 
 }  // namespace
@@ -125,12 +171,14 @@ void help() {
 int main(int argc, char **argv) {
     std::string dtype = "f32", dir = getenv("BRD_DATA_DIR") ? getenv("BRD_DATA_DIR") : "data",
                 csv = "data/cuda_2_benchmark.csv";
+    int band = 32;
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         if (a == "--dtype" && i + 1 < argc) dtype = argv[++i];
         else if (a == "--data-dir" && i + 1 < argc) dir = argv[++i];
         else if (a == "--csv" && i + 1 < argc) csv = argv[++i];
+        else if (a == "--band" && i + 1 < argc) band = std::atoi(argv[++i]);
         else pos.push_back(a);
     }
     if (pos.size() >= 2 && pos[0] == "check") {
@@ -141,6 +189,10 @@ int main(int argc, char **argv) {
         const int step = std::atoi(pos[1].c_str()), ns = std::atoi(pos[2].c_str()), ni = std::atoi(pos[3].c_str()),
                   b = std::atoi(pos[4].c_str());
         return dtype == "f64" ? benchmark<double>(step, ns, ni, b, csv) : benchmark<float>(step, ns, ni, b, csv);
+    }
+    if (pos.size() >= 2 && pos[0] == "svd") {
+        const int n = std::atoi(pos[1].c_str());
+        return dtype == "f64" ? svd<double>(n, band) : svd<float>(n, band);
     }
     help();
     return 0;

@@ -286,3 +286,16 @@ def test_one_stage_band1_is_bidiagonal_with_input_singular_values(S, T):
     sv = S.bdsvd(np.diagonal(B).copy(), np.diagonal(B, 1).copy())
     ref = np.linalg.svd(A.astype(np.float64), compute_uv=False)
     assert np.max(np.abs(sv.astype(np.float64) - ref)) / ref[0] < (1e-12 if T == "double" else 1e-5)
+
+
+def test_cli_svd_runs(S):
+    """svd_gpu svd: the C++ caller of the whole pipeline (stage 1, sigma stage 2,
+    brd_bdsvd) runs and prints descending singular values."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(S.LIB_PATH), "..", "bin", "svd_gpu")
+    out = subprocess.run([exe, "svd", "512", "--dtype", "f64"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("largest")][0]
+    vals = [float(x) for x in line.split(":")[1].split()]
+    assert len(vals) == 5 and all(a >= b for a, b in zip(vals, vals[1:])) and vals[0] > 0

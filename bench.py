@@ -100,7 +100,7 @@ def cpu_baseline(n: int, band: int) -> dict:
             "kind": kind, "sample": f"one {n}x{n} fp64 two-stage reduction, b={band}, {dt:.2f} s"}
 
 
-def pmc_traffic(kernel_prefix: str):
+def pmc_traffic(*kernel_prefixes: str):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
     (tools/pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled
     for gfx950's 64-B tally of 128-B requests, MI355X_MICROARCH.md 'HBM').  The
@@ -112,7 +112,7 @@ def pmc_traffic(kernel_prefix: str):
         return None, None
     tot, cnt = 0.0, 0
     for line in open(files[-1]):
-        if line.startswith(kernel_prefix):
+        if line.startswith(kernel_prefixes):
             f = line.split()
             try:
                 d, two_fetch, wr = int(f[-4]), float(f[-2]), float(f[-1])
@@ -124,14 +124,16 @@ def pmc_traffic(kernel_prefix: str):
 
 
 def apply_roofline(ap, dtype):
-    """Stage-1 trailing update (k_apply): per element of the trailing matrix one
-    read + one write against 4b flops -> 8 flop/B at b = 32 fp64, below the
-    MFMA ridge (78.6 TF / 8 TB/s = 9.8 flop/B): HBM-bound."""
+    """Stage-1 trailing update (k_apply, and k_apply_factor: the same apply with
+    the next tree level's factor in one extra workgroup): per element of the
+    trailing matrix one read + one write against 4b flops -> 8 flop/B at b = 32
+    fp64, below the MFMA ridge (78.6 TF / 8 TB/s = 9.8 flop/B): HBM-bound."""
     ms, launches = ap["ms"], max(ap["launches"], 1)
     gbs = ap["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tf = ap["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-    traffic, src = pmc_traffic("void brd::k_apply<" + ("double" if dtype == "f64" else "float"))
-    return {"kernel": "k_apply (stage-1 trailing update, MFMA)", "bound": "hbm",
+    tn = "double" if dtype == "f64" else "float"
+    traffic, src = pmc_traffic("void brd::k_apply<" + tn, "void brd::k_apply_factor<" + tn)
+    return {"kernel": "k_apply + k_apply_factor (stage-1 trailing update, MFMA)", "bound": "hbm",
             "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,
             "algorithmic_bytes_per_launch": round(ap["bytes"] / launches),

@@ -101,8 +101,6 @@ struct Ctx {
     bool have_user_stream = false;   // true: use user_stream (NULL = legacy default stream)
     hipStream_t user_stream = nullptr;
     hipStream_t own_stream = nullptr;
-    hipStream_t side_stream = nullptr;   // stage 1: root-level factors beside the leaf apply
-    hipEvent_t ev_leaf = nullptr, ev_root = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0;
     int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
@@ -119,15 +117,6 @@ static hipStream_t stream() {
     if (g_ctx.have_user_stream) return g_ctx.user_stream;
     if (!g_ctx.own_stream) hipStreamCreateWithFlags(&g_ctx.own_stream, hipStreamNonBlocking);
     return g_ctx.own_stream;
-}
-
-static int ensure_side() {
-    if (g_ctx.side_stream) return BRD_OK;
-    if (hipStreamCreateWithFlags(&g_ctx.side_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&g_ctx.ev_leaf, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g_ctx.ev_root, hipEventDisableTiming) != hipSuccess)
-        return fail(BRD_EHIP, "stage-1 side stream / events could not be created");
-    return BRD_OK;
 }
 
 static int ensure_ws(size_t bytes) {
@@ -251,9 +240,9 @@ long tree_level_rows(const Tree &t, int level) {
 // One side (QR of a column panel + left update, or LQ of a row panel + right
 // update) of panel k.  The reduction tree's upper levels depend only on the
 // leaves' R factors (panel columns) and the leaf-level apply only on the
-// leaves' V, T (trailing columns), so the upper-level factors run on the side
-// stream while the leaf apply runs on the main stream; the upper-level applies
-// wait for both.
+// leaves' V, T (trailing columns), so each apply launch also runs the next
+// level's factor (k_apply_factor): factor L0, then [apply L0 + factor L1],
+// [apply L1 + factor L2], ... on one stream, with no event hand-offs.
 template <typename T>
 static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &ws, T *X, int ncols,
                       hipStream_t s) {
@@ -261,28 +250,19 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
         ProfScope ps("s1_factor", 0, 0, s);
         HIP_TRY(launch_factor<T>(trans, P, lda, t, 0, ws, s));
     }
-    static const char *ov = getenv("BRD_S1_OVERLAP");   // tuning: "0" = no side stream
-    const bool split = t.nlevels > 1 && ncols > 0 && !(ov && ov[0] == '0');
-    if (split) {
-        HIP_TRY(hipEventRecord(g_ctx.ev_leaf, s));
-        HIP_TRY(hipStreamWaitEvent(g_ctx.side_stream, g_ctx.ev_leaf, 0));
-    }
-    hipStream_t sf = split ? g_ctx.side_stream : s;
-    for (int l = 1; l < t.nlevels; ++l) {
-        ProfScope ps("s1_factor", 0, 0, sf);
-        HIP_TRY(launch_factor<T>(trans, P, lda, t, l, ws, sf));
+    static const char *ov = getenv("BRD_S1_OVERLAP");   // tuning: "0" = factors and applies as separate launches
+    const bool fuse = ncols > 0 && !(ov && ov[0] == '0');
+    if (!fuse) {
+        for (int l = 1; l < t.nlevels; ++l) {
+            ProfScope ps("s1_factor", 0, 0, s);
+            HIP_TRY(launch_factor<T>(trans, P, lda, t, l, ws, s));
+        }
     }
     if (ncols <= 0) return BRD_OK;
     for (int l = 0; l < t.nlevels; ++l) {
-        if (l == 1 && split) {
-            HIP_TRY(hipEventRecord(g_ctx.ev_root, sf));
-            HIP_TRY(hipStreamWaitEvent(s, g_ctx.ev_root, 0));
-        }
         const double rows = (double)tree_level_rows(t, l);
         ProfScope ps("s1_apply", 4.0 * t.bk * rows * ncols, 2.0 * rows * ncols * sizeof(T), s);
-        static const char *fe = getenv("BRD_S1_FREE");   // tuning: CUs left free beside the leaf apply
-        const int free_cus = fe ? atoi(fe) : 16;
-        HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, l == 0 && split ? 256 - free_cus : 256));
+        HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, 256, fuse ? P : nullptr));
     }
     return BRD_OK;
 }
@@ -292,8 +272,6 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
     int rc = ensure_ws(need);
-    if (rc) return rc;
-    rc = ensure_side();
     if (rc) return rc;
     TreeWs ws;
     for (int k = 0; k < n; k += b) {

@@ -298,24 +298,27 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
         D_TRY(C.bcast(Pbuf, (size_t)mp * bk * sz, owner, s));
         const Tree tq = make_tree(mp, bk);
         tree_ws_carve(tq, sz, wsmain, ws);
-        for (int l = 0; l < tq.nlevels; ++l) {
+        // with trailing columns here, the upper tree levels are factored inside
+        // the apply launches (k_apply_factor), as in the one-GPU driver
+        const bool fuse = n2 > 0 && nc > 0;
+        for (int l = 0; l < (fuse ? 1 : tq.nlevels); ++l) {
             void *h = api_prof_begin("s1_factor", 0, 0, s);
             D_HIP(launch_factor<T>(false, Pbuf, bk, tq, l, ws, s));
             api_prof_end(h, s);
         }
-        if (me == owner)
-            D_HIP(hipMemcpy2DAsync(A + (long)kb * lda + lc_k, lda * sz, Pbuf, bk * sz, bk * sz, mp,
-                                   hipMemcpyDeviceToDevice, s));
         // ---- 2. left update of my trailing columns
-        if (n2 <= 0) continue;
-        if (nc > 0) {
+        if (fuse) {
             for (int l = 0; l < tq.nlevels; ++l) {
                 const double rows = (double)tree_level_rows(tq, l);
                 void *h = api_prof_begin("s1_apply", 4.0 * bk * rows * nc, 2.0 * rows * nc * sz, s);
-                D_HIP(launch_apply<T>(false, A + (long)kb * lda + lcs, lda, tq, l, nc, ws, s));
+                D_HIP(launch_apply<T>(false, A + (long)kb * lda + lcs, lda, tq, l, nc, ws, s, 256, Pbuf, bk));
                 api_prof_end(h, s);
             }
         }
+        if (me == owner)   // the factored panel (R, zeros below) back into my columns
+            D_HIP(hipMemcpy2DAsync(A + (long)kb * lda + lc_k, lda * sz, Pbuf, bk * sz, bk * sz, mp,
+                                   hipMemcpyDeviceToDevice, s));
+        if (n2 <= 0) continue;
         // ---- 3. LQ of the row panel: local tree, gathered stacked R, root
         T *Q = A + (long)kb * lda + lcs;   // TR view: logical rows = my trailing columns
         Tree tl{};

@@ -51,11 +51,13 @@ void tree_ws_carve(const Tree &t, size_t elem, void *base, TreeWs &ws);
 template <typename T>
 hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
                          const TreeWs &ws, hipStream_t s);
-// target: workgroups to aim for (about one per CU; fewer leaves CUs free for
-// a factor kernel running beside the apply).
+// target: workgroups to aim for (about one per CU).  fuse_panel / fuse_ld:
+// the panel (factor view base, leading dimension; 0 = ld) whose level+1
+// factor runs in the same launch (k_apply_factor), when the tree has that level.
 template <typename T>
 hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
-                        int ncols, const TreeWs &ws, hipStream_t s, int target = 256);
+                        int ncols, const TreeWs &ws, hipStream_t s, int target = 256,
+                        T *fuse_panel = nullptr, long fuse_ld = 0);
 
 // Stage-2 launchers (brd_stage2.hip).
 template <typename T>

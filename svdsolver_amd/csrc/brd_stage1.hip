@@ -251,20 +251,31 @@ __device__ __forceinline__ Reflector<T> make_reflector(T sub2, T x0) {
     return h;
 }
 
-template <typename T, bool TR>
-__global__ void __launch_bounds__(kFT)
-k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__restrict__ VTws,
-         T *__restrict__ Tws)
-{
-    __shared__ T sV[2][kRmax];        // published reflector column (raw, rows > j), double-buffered
-    __shared__ T sH[2][4];            // its 1/u1, tau, alpha
-    __shared__ T sZ[32][33];          // v_c^T v_j (c < j)
-    __shared__ T sT[32][33];
-    __shared__ T sU1[32], sTau[32];   // 1/u1 and tau per column
-    __shared__ int sMap[kRmax];
-    __shared__ T sStage[kRmax / 2][33];   // row-major <-> register-layout staging, half a node at a time
+template <typename T>
+struct FactorLds {
+    T sV[2][kRmax];        // published reflector column (raw, rows > j), double-buffered
+    T sH[2][4];            // its 1/u1, tau, alpha
+    T sZ[32][33];          // v_c^T v_j (c < j)
+    T sT[32][33];
+    T sU1[32], sTau[32];   // 1/u1 and tau per column
+    int sMap[kRmax];
+    T sStage[kRmax / 2][33];   // row-major <-> register-layout staging, half a node at a time
+};
 
-    const int grp = blockIdx.x;
+// The factor of node grp (k_factor, or the factor role of k_apply_factor).
+template <typename T, bool TR>
+__device__ __forceinline__ void factor_body(FactorLds<T> &L, const int grp, T *__restrict__ base, long ld, LvArgs la,
+                                            T *__restrict__ Vws, T *__restrict__ VTws, T *__restrict__ Tws)
+{
+    auto &sV = L.sV;
+    auto &sH = L.sH;
+    auto &sZ = L.sZ;
+    auto &sT = L.sT;
+    auto &sU1 = L.sU1;
+    auto &sTau = L.sTau;
+    auto &sMap = L.sMap;
+    auto &sStage = L.sStage;
+
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -471,6 +482,15 @@ k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__res
     STAMP(6);
 }
 
+template <typename T, bool TR>
+__global__ void __launch_bounds__(kFT)
+k_factor(T *__restrict__ base, long ld, LvArgs la, T *__restrict__ Vws, T *__restrict__ VTws,
+         T *__restrict__ Tws)
+{
+    __shared__ FactorLds<T> L;
+    factor_body<T, TR>(L, blockIdx.x, base, ld, la, Vws, VTws, Tws);
+}
+
 // ==========================================================================
 // k_apply: X <- X - V (T^T (V^T X)) for one tree node (rows = the node's row
 // list, <= kRmax) and a run of kASlab-wide column slabs.
@@ -503,19 +523,36 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Slab staging.  TR = false: thread -> column tid%16, rows tid/16 + 32p.
-// TR = true: thread -> row tid (< kRmax), all 16 columns.
+// Slab staging.  TR = false: thread -> element pair 2(tid%8), 2(tid%8)+1 of
+// rows tid/8 + 64p (one 16-byte load per row for fp64, 8 threads per 128-byte
+// row); TR = true: thread -> row tid (< kRmax), all 16 columns.  The
+// write-back (slab_store) uses the same map, so the row addresses are shared.
+constexpr int kXP = kXN / 2;   // TR = false: element pairs per thread
+
+template <typename T>
+struct Pair {
+    typedef T v2 __attribute__((ext_vector_type(2), aligned(sizeof(T))));
+};
+
 template <typename T, bool TR>
 __device__ __forceinline__ void slab_load(const T *base, long ld, const int *sMap, int nr, int c0, int nc,
                                           int tid, T (&xn)[kXN]) {
     if (!TR) {
-        const int cc = tid & (kASlab - 1);
+        typedef typename Pair<T>::v2 v2;
+        const int c2 = 2 * (tid & 7);
 #pragma unroll
-        for (int p = 0; p < kXN; ++p) {
-            const int r = (tid / kASlab) + (kAT / kASlab) * p;
-            const bool ok = r < nr && cc < nc;
+        for (int p = 0; p < kXP; ++p) {
+            const int r = (tid >> 3) + (kAT / 8) * p;
+            const bool ok = r < nr && c2 < nc;
             const int pr = ok ? sMap[r] : 0;
-            xn[p] = ok ? base[(long)pr * ld + c0 + cc] : (T)0;
+            v2 v = {(T)0, (T)0};
+            if (ok) {
+                const T *src = base + (long)pr * ld + c0 + c2;
+                if (c2 + 1 < nc) v = *(const v2 *)src;
+                else v.x = src[0];
+            }
+            xn[2 * p] = v.x;
+            xn[2 * p + 1] = v.y;
         }
     } else {
         const int r = tid;
@@ -529,11 +566,12 @@ __device__ __forceinline__ void slab_load(const T *base, long ld, const int *sMa
 template <typename T, bool TR>
 __device__ __forceinline__ void slab_to_lds(T *sX, int nrp, int tid, const T (&xn)[kXN]) {
     if (!TR) {
-        const int cc = tid & (kASlab - 1);
+        typedef typename Pair<T>::v2 v2;
+        const int c2 = 2 * (tid & 7);
 #pragma unroll
-        for (int p = 0; p < kXN; ++p) {
-            const int r = (tid / kASlab) + (kAT / kASlab) * p;
-            if (r < nrp) sX[xidx<false>(r, cc)] = xn[p];
+        for (int p = 0; p < kXP; ++p) {
+            const int r = (tid >> 3) + (kAT / 8) * p;
+            if (r < nrp) *(v2 *)&sX[xidx<false>(r, c2)] = v2{xn[2 * p], xn[2 * p + 1]};
         }
     } else {
         const int r = tid;
@@ -544,21 +582,59 @@ __device__ __forceinline__ void slab_to_lds(T *sX, int nrp, int tid, const T (&x
     }
 }
 
+// Updated slab: LDS -> matrix, coalesced (TR = false: the slab_load map;
+// TR = true: consecutive threads -> consecutive physical columns).
 template <typename T, bool TR>
-__global__ void __launch_bounds__(kAT)
-k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
-        const T *__restrict__ VTws, const T *__restrict__ Tws)
+__device__ __forceinline__ void slab_store(T *base, long ld, const int *sMap, int nr, int c0, int nc, int tid,
+                                           const T *sX) {
+    if (!TR) {
+        typedef typename Pair<T>::v2 v2;
+        const int c2 = 2 * (tid & 7);
+#pragma unroll
+        for (int p = 0; p < kXP; ++p) {
+            const int r = (tid >> 3) + (kAT / 8) * p;
+            if (r < nr && c2 < nc) {
+                const v2 v = *(const v2 *)&sX[xidx<false>(r, c2)];
+                T *dst = base + (long)sMap[r] * ld + c0 + c2;
+                if (c2 + 1 < nc) *(v2 *)dst = v;
+                else dst[0] = v.x;
+            }
+        }
+    } else {
+        const int r = tid;
+        if (r < nr) {
+            const int pr = sMap[r];
+#pragma unroll
+            for (int k = 0; k < kXN; ++k)
+                if (k < nc) base[(long)(c0 + k) * ld + pr] = sX[xidx<true>(r, k)];
+        }
+    }
+}
+
+template <typename T>
+struct ApplyLds {
+    T sX[kASlab * kPT];
+    T sW[32 * 17];
+    T sW2[32 * 17];
+    T sT[32 * 32];
+    int sMap[kRmax];
+};
+
+// The apply of node grp to slab run `run` (k_apply, or the apply role of k_apply_factor).
+template <typename T, bool TR>
+__device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const int run, T *__restrict__ base, long ld,
+                                           LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
+                                           const T *__restrict__ VTws, const T *__restrict__ Tws)
 {
     typedef typename Mfma<T>::v4 v4;
-    __shared__ T sX[kASlab * kPT];
-    __shared__ T sW[32 * 17];
-    __shared__ T sW2[32 * 17];
-    __shared__ T sT[32 * 32];
-    __shared__ int sMap[kRmax];
+    auto &sX = L.sX;
+    auto &sW = L.sW;
+    auto &sW2 = L.sW2;
+    auto &sT = L.sT;
+    auto &sMap = L.sMap;
 
-    const int grp = blockIdx.x;
     const int nslabs = (ncols + kASlab - 1) / kASlab;
-    const int s0 = blockIdx.y * spw, s1 = min(nslabs, s0 + spw);
+    const int s0 = run * spw, s1 = min(nslabs, s0 + spw);
     if (s0 >= s1) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l15 = lane & 15;
@@ -653,36 +729,54 @@ k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *_
 #pragma unroll
                     for (int s = 0; s < 8; ++s)
                         if (s < ksteps) acc = Mfma<T>::mma(Vu[jb][s], bw[s], acc);
-                    if (!TR) {
-                        // straight to HBM: 4 rows x 16 consecutive elements per store
 #pragma unroll
-                        for (int g = 0; g < 4; ++g) {
-                            const int r = blk * 16 + q + 4 * g;
-                            if (r < nr && l15 < nc) base[(long)sMap[r] * ld + c0 + l15] = acc[g];
-                        }
-                    } else {
-#pragma unroll
-                        for (int g = 0; g < 4; ++g) sX[xidx<TR>(blk * 16 + q + 4 * g, l15)] = acc[g];
-                    }
+                    for (int g = 0; g < 4; ++g) sX[xidx<TR>(blk * 16 + q + 4 * g, l15)] = acc[g];
                 }
             }
         }
         lds_barrier();
-        if (TR) {   // coalesced write-back: consecutive threads -> consecutive physical columns
-            const int r = tid;
-            if (r < nr) {
-                const int pr = sMap[r];
-#pragma unroll
-                for (int k = 0; k < kXN; ++k)
-                    if (k < nc) base[(long)(c0 + k) * ld + pr] = sX[xidx<true>(r, k)];
-            }
-            lds_barrier();
-        }
+        slab_store<T, TR>(base, ld, sMap, nr, c0, nc, tid, sX);
+        lds_barrier();
         if (slab + 1 < s1) {
             slab_to_lds<T, TR>(sX, nrp, tid, xn);
             lds_barrier();
         }
     }
+}
+
+template <typename T, bool TR>
+__global__ void __launch_bounds__(kAT)
+k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
+        const T *__restrict__ VTws, const T *__restrict__ Tws)
+{
+    __shared__ ApplyLds<T> L;
+    apply_body<T, TR>(L, blockIdx.x, blockIdx.y, base, ld, la, ncols, spw, Vws, VTws, Tws);
+}
+
+// k_apply_factor: the apply of tree level l (blockIdx.y >= 1) and the factor
+// of level l+1 (blockIdx.y = 0, blockIdx.x < nfac) in one launch.  The
+// level-(l+1) factor reads only the level-l nodes' R rows of the panel and
+// writes only level-(l+1) workspace, the apply only the trailing columns and
+// level-l workspace, so the two roles are independent; fusing them replaces
+// the side stream and its two event hand-offs per panel side (about 6-7 us of
+// idle GPU each, measured).  Row y = 0 is dispatched first, so the factor
+// starts at once on a CU of its own.
+template <typename T, bool TR>
+__global__ void __launch_bounds__(kAT)
+k_apply_factor(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
+               const T *__restrict__ VTws, const T *__restrict__ Tws, T *__restrict__ fbase, long fld, LvArgs fa,
+               int nfac, T *__restrict__ fV, T *__restrict__ fVT, T *__restrict__ fT)
+{
+    static_assert(kAT == kFT, "one block size for both roles");
+    __shared__ union Lds {
+        FactorLds<T> f;
+        ApplyLds<T> a;
+    } L;
+    if (blockIdx.y == 0) {
+        if ((int)blockIdx.x < nfac) factor_body<T, TR>(L.f, blockIdx.x, fbase, fld, fa, fV, fVT, fT);
+        return;
+    }
+    apply_body<T, TR>(L.a, blockIdx.x, blockIdx.y - 1, base, ld, la, ncols, spw, Vws, VTws, Tws);
 }
 
 // --------------------------------------------------------------------------
@@ -716,17 +810,32 @@ hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
 
 template <typename T>
 hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, int ncols,
-                        const TreeWs &ws, hipStream_t s, int target)
+                        const TreeWs &ws, hipStream_t s, int target, T *fuse_panel, long fuse_ld)
 {
     if (ncols <= 0) return hipSuccess;
     LvArgs a = lv_args(t, level);
     const int groups = t.lv[level].groups;
     const int nslabs = (ncols + kASlab - 1) / kASlab;
+    const bool fuse = fuse_panel && level + 1 < t.nlevels;
+    const int nfac = fuse ? t.lv[level + 1].groups : 0;
     // one resident workgroup per CU (registers): aim for about one wave of
-    // `target` workgroups (fewer than the CUs leaves room for a concurrent factor)
-    const int spw = std::max(1, (groups * nslabs + target - 1) / target);
-    dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
+    // `target` workgroups, less the CUs the fused factor takes
+    const int tgt = std::max(1, target - nfac);
+    const int spw = std::max(1, (groups * nslabs + tgt - 1) / tgt);
     const T *V = (const T *)ws.V[level], *VT = (const T *)ws.VT[level], *Tm = (const T *)ws.T[level];
+    if (fuse) {
+        dim3 grid(groups, 1 + (nslabs + spw - 1) / spw), block(kAT);
+        const LvArgs fa = lv_args(t, level + 1);
+        T *fV = (T *)ws.V[level + 1], *fVT = (T *)ws.VT[level + 1], *fT = (T *)ws.T[level + 1];
+        if (trans)
+            hipLaunchKernelGGL((k_apply_factor<T, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+                               fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+        else
+            hipLaunchKernelGGL((k_apply_factor<T, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+                               fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+        return hipGetLastError();
+    }
+    dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
     if (trans)
         hipLaunchKernelGGL((k_apply<T, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
     else
@@ -736,7 +845,7 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
 
 template hipError_t launch_factor<double>(bool, double *, long, const Tree &, int, const TreeWs &, hipStream_t);
 template hipError_t launch_factor<float>(bool, float *, long, const Tree &, int, const TreeWs &, hipStream_t);
-template hipError_t launch_apply<double>(bool, double *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int);
-template hipError_t launch_apply<float>(bool, float *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int);
+template hipError_t launch_apply<double>(bool, double *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int, double *, long);
+template hipError_t launch_apply<float>(bool, float *, long, const Tree &, int, int, const TreeWs &, hipStream_t, int, float *, long);
 
 }  // namespace brd

@@ -91,6 +91,27 @@ def test_stage1_orthogonal_invariants(S, T):
 
 
 @pytest.mark.parametrize("T", ["double", "float"])
+def test_stage1_tall_three_level_tree(S, T):
+    """m = 9000 > 16 * 512 rows: the column panels' reduction trees have three
+    levels, so the level-2 factor runs inside the level-1 apply launch
+    (k_apply_factor) -- the N = 16384 shape, at a size numpy checks in
+    seconds.  Exact zeros outside the band (m x n, upper band), singular
+    values and Frobenius norm preserved."""
+    rng = np.random.default_rng(11)
+    m, n, b = 9000, 96, 32
+    dt = np.float64 if T == "double" else np.float32
+    A = rng.uniform(0, 5, (m, n)).astype(dt)
+    B = S.brd_p1(A, b)
+    i, j = np.indices((m, n))
+    assert np.all(B[(j < i) | (j - i > b)] == 0)
+    sa = np.linalg.svd(A.astype(np.float64), compute_uv=False)
+    sb = np.linalg.svd(B.astype(np.float64), compute_uv=False)
+    assert np.max(np.abs(sa - sb)) / sa[0] < (1e-12 if T == "double" else 2e-5)
+    fa, fb = np.linalg.norm(A.astype(np.float64)), np.linalg.norm(B.astype(np.float64))
+    assert abs(fa - fb) / fa < (1e-12 if T == "double" else 1e-5)
+
+
+@pytest.mark.parametrize("T", ["double", "float"])
 def test_stage2_exact_order_bit_identical_64(S, T):
     band = G.ref_bin(f"band_{T}_64_64.bin", 64, T)
     out, d, e = S.brd_p2(band, 4, exact_order=True)

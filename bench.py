@@ -58,6 +58,11 @@ def parse():
                         "sigma-preserving variant (BRD_SIGMA)")
     p.add_argument("--mode", choices=["dist", "replicas"], default="dist",
                    help="N > 1: sharded stage 1 of one matrix (dist) or independent replicas")
+    p.add_argument("--pipeline", choices=["on", "off"], default="on",
+                   help="on: stage 2 of matrix i runs on a second HIP stream beside stage 1 of "
+                        "matrix i+1 (a stream of independent reductions); off: one reduction at a time")
+    p.add_argument("--s2-cus", type=int, default=None,
+                   help="pipelined: CUs reserved for stage 2 (default svdsolver_amd.overlap_cus(n))")
     p.add_argument("--force-dist", action="store_true",
                    help="run the distributed path even at world size 1 (launch through torch.distributed.run)")
     return p.parse_args()
@@ -187,7 +192,11 @@ def main():
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     nmat = args.warmup + 2 * args.steps   # warmup, the timed steps, the profiled steps
     dist_mode = (world > 1 or args.force_dist) and args.mode == "dist"
-    stream = torch.cuda.current_stream(dev)
+    pipelined = args.pipeline == "on"
+    s2_cus = S.overlap_cus(n) if pipelined else 0
+    if args.s2_cus is not None:
+        s2_cus = args.s2_cus
+    S.set_overlap(s2_cus)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     if dist_mode:
@@ -196,53 +205,92 @@ def main():
         n_loc = D.local_cols(n, b, world, rank)
         base = torch.rand((n, max(n_loc, 1)), dtype=tdt, device=dev, generator=g)[:, :n_loc] * 5.0
         mats = [base.contiguous().clone() for _ in range(nmat)]
-        Bfull = torch.empty((n, n), dtype=tdt, device=dev) if rank == 0 else None
+        # Matrix j's band goes to rank j mod world, which runs its stage 2; two
+        # band buffers per rank so a gather never lands in a band whose sweep
+        # may still be running (the stage-1 stream also waits for that sweep).
+        Bfull = [torch.empty((n, n), dtype=tdt, device=dev) for _ in range(2 if pipelined else 1)]
+        s2_done = [None] * len(Bfull)
 
-        def stage1(A):
+        def root_of(j):
+            return j % world if pipelined else 0
+
+        def band_of(j):
+            return (j // world) % len(Bfull)
+
+        def stage1(A, j):
             D.ge2band(A, n, b, sync=False)
-            D.gather_band(A, n, b, root=0, out=Bfull, sync=False)
+            r, k = root_of(j), band_of(j)
+            if rank == r and s2_done[k] is not None:
+                torch.cuda.current_stream(dev).wait_event(s2_done[k])
+            D.gather_band(A, n, b, root=r, out=Bfull[k] if rank == r else None, sync=False)
 
-        def stage2(A):
-            if rank == 0:
-                S.band2bd(Bfull, b, sigma=args.s2 == "sigma", sync=False, extract=False)
+        def stage2(A, j):
+            if rank == root_of(j):
+                k = band_of(j)
+                S.band2bd(Bfull[k], b, sigma=args.s2 == "sigma", sync=False, extract=False)
+                e = torch.cuda.Event()
+                e.record(torch.cuda.current_stream(dev))
+                s2_done[k] = e
     else:
         base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
         mats = [base.clone() for _ in range(nmat)]
 
-        def stage1(A):
+        def stage1(A, j):
             S.ge2band(A, b, sync=False)
 
-        def stage2(A):
+        def stage2(A, j):
             S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
+    # Two launch streams: stage 1 (and the band gather) on s_a, stage 2 on s_b.
+    # Pipelined, stage 2 of matrix i waits only for stage 1 of matrix i, so it
+    # runs beside stage 1 of matrix i+1 (stage 2 is a latency-bound chain on a
+    # few dozen CUs, stage 1 HBM-bound on the rest); otherwise s_b's work is
+    # ordered after all of s_a's and vice versa (one reduction at a time).
+    s_a, s_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
-    for i in range(args.warmup):
-        stage1(mats[i])
-        stage2(mats[i])
+    def issue(first, count, ev=None):
+        last = None
+        for i in range(count):
+            j = first + i
+            A = mats[j]
+            with torch.cuda.stream(s_a):
+                if not pipelined and last is not None:
+                    s_a.wait_event(last)
+                if ev:
+                    ev[i][0].record(s_a)
+                stage1(A, j)
+                e1 = torch.cuda.Event(enable_timing=bool(ev))
+                e1.record(s_a)
+            with torch.cuda.stream(s_b):
+                s_b.wait_event(e1)
+                if ev:
+                    ev[i][1].record(s_b)
+                stage2(A, j)
+                last = torch.cuda.Event(enable_timing=bool(ev))
+                last.record(s_b)
+                if ev:
+                    ev[i][2] = (e1, last)
+
+    issue(0, args.warmup)
     torch.cuda.synchronize(dev)
 
     def run_steps(first):
         """K steps bracketed by barrier + synchronize; per-step stage split by
         events on the launch stream.  Returns (elapsed, stage1 ms, stage2 ms)."""
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), None]
+              for _ in range(args.steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            A = mats[first + i]
-            ev[i][0].record(stream)
-            stage1(A)
-            ev[i][1].record(stream)
-            stage2(A)
-            ev[i][2].record(stream)
+        issue(first, args.steps, ev)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        return (el, sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps,
-                sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps)
+        s2 = [e[1].elapsed_time(e[2][1]) for i, e in enumerate(ev) if not dist_mode or rank == root_of(first + i)]
+        return (el, sum(e[0].elapsed_time(e[2][0]) for e in ev) / args.steps,
+                sum(s2) / max(1, len(s2)))
 
     # (1) the timed steps: `value` (no per-launch instrumentation inside)
     elapsed, s1, s2 = run_steps(args.warmup)
@@ -281,8 +329,13 @@ def main():
                                    + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
                                       else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
                        "n": n, "band": b, "global_batch": matrices,
-                       "parallelism": (f"stage1 block-cyclic columns over {world} GPUs (RCCL), stage2 rank 0"
-                                       if dist_mode else f"replicas{world}")},
+                       "parallelism": (f"stage1 block-cyclic columns over {world} GPUs (RCCL), stage2 on rank "
+                                       + ("(matrix index mod world)" if pipelined else "0")
+                                       if dist_mode else f"replicas{world}"),
+                       "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
+                                    if pipelined else "off: one reduction at a time"),
+                       "stage2_cus": s2_cus or "all"},
+            "latency_ms_per_reduction": round(s1 + s2, 3),
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
             "roofline": apply_roofline(ap, args.dtype),

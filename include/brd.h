@@ -80,6 +80,15 @@ int brd_bdsvd_f32(const float *d, const float *e, int n, float *sv);
 int brd_set_stream(void *hip_stream);
 int brd_use_own_stream(void);
 
+/* Two reductions side by side (a stream of matrices): stage 2 of matrix i on
+ * one stream while stage 1 of matrix i+1 runs on another.  s2_cus > 0 runs
+ * every stage-2 sweep on that many workgroups (one per CU; the bundle chain
+ * keeps fewer than ~64 busy at N <= 16384) and sizes stage-1 launches for the
+ * remaining CUs; 0 restores the defaults (each stage on the whole chip).
+ * No reference counterpart (the reference runs one reduction at a time,
+ * svd_cuda_2.cu:1387 / timing.h:55). */
+int brd_set_overlap(int s2_cus);
+
 /* Per-kernel device timing for roofline reporting.  While enabled, the library
  * brackets every launch of the named kernel class with HIP events on the
  * launch stream.  kernel: "s1_apply", "s1_factor", "s2_sweep".  Returns the

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -37,7 +37,7 @@ BRD_SIGMA = 0x10
 
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
-    "brd_set_stream", "brd_use_own_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
+    "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
     "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
     "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_last_error", "brd_version",
@@ -78,6 +78,8 @@ def _load() -> ctypes.CDLL:
     L.brd_set_stream.restype = ci
     L.brd_use_own_stream.argtypes = []
     L.brd_use_own_stream.restype = ci
+    L.brd_set_overlap.argtypes = [ci]
+    L.brd_set_overlap.restype = ci
     L.brd_profile_enable.argtypes = [ci]
     L.brd_profile_enable.restype = ci
     L.brd_profile_reset.argtypes = []
@@ -242,6 +244,61 @@ def singular_values(A, b: int = 32):
     B = brd_p1(A, b)
     _, d, e = brd_p2(B, b, sigma=True)
     return bdsvd(d, e)
+
+
+# ---------------------------------------------------------------------------
+# stream of reductions: stage 2 of one matrix beside stage 1 of the next
+# ---------------------------------------------------------------------------
+def set_overlap(s2_cus: int) -> None:
+    """brd_set_overlap (include/brd.h): run stage-2 sweeps on ``s2_cus``
+    workgroups and size stage-1 launches for the remaining CUs, so that a
+    band2bd on one stream and a ge2band on another share the chip; 0 restores
+    the whole-chip defaults."""
+    _check("brd_set_overlap", lib.brd_set_overlap(int(s2_cus)))
+
+
+def overlap_cus(n: int) -> int:
+    """CUs reserved for stage 2 when it overlaps stage 1.  Measured on MI355X
+    (profiles/README.md, pipelined bench at n = 8192): 32 workgroups keep the
+    sweep chain within 1 % of its whole-chip time and leave 224 CUs (28 per
+    XCD) to stage 1 (93.7 ms beside the sweep, 88 ms alone); 64 gave 101.7 ms,
+    and 40-56 or 72-128 were slower still.  Stage 1 dominates at larger n, so
+    the reservation stays at 32."""
+    return 32 if n >= 1024 else 16
+
+
+def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = None, sync: bool = True):
+    """Two-stage reduction of a sequence of square CUDA tensors, each in place,
+    pipelined over two HIP streams: stage 2 of matrix i (its own stream,
+    ``s2_cus`` workgroups) runs beside stage 1 of matrix i+1 (the other
+    stream, sized for the remaining CUs).  Returns [(d, e)] per matrix (device
+    tensors).  Each matrix sees exactly the calls of ge2band + band2bd; only
+    their overlap differs.  The library's overlap setting is restored on exit.
+    """
+    import torch
+    if not mats:
+        return []
+    dev = mats[0].device
+    cus = overlap_cus(mats[0].shape[0]) if s2_cus is None else int(s2_cus)
+    s_a, s_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s_a.wait_stream(torch.cuda.current_stream(dev))
+    out = []
+    set_overlap(cus)
+    try:
+        for A in mats:
+            with torch.cuda.stream(s_a):
+                ge2band(A, b, sync=False)
+                done1 = torch.cuda.Event()
+                done1.record(s_a)
+            with torch.cuda.stream(s_b):
+                s_b.wait_event(done1)
+                out.append(band2bd(A, b, sigma=sigma, sync=False))
+    finally:
+        set_overlap(0)
+    torch.cuda.current_stream(dev).wait_stream(s_b)
+    if sync:
+        torch.cuda.synchronize(dev)
+    return out
 
 
 # ---------------------------------------------------------------------------

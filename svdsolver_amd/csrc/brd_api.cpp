@@ -106,6 +106,7 @@ struct Ctx {
     int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
     int s2_cap = 0;
     int *s2_err_host = nullptr;  // pinned copy of the error word
+    int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
     std::map<std::string, ProfAcc> acc;
     std::vector<Pending> pending;
@@ -148,13 +149,37 @@ static int ensure_s2_flags(int n) {
     return BRD_OK;
 }
 
-static int s2_waves() {
-    static int nw = 0;
-    if (!nw) {
-        int dev = 0, cus = 256;
+static int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        cus = 256;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        nw = std::max(64, cus);
+    }
+    return cus;
+}
+
+// Workgroups a stage-1 apply launch is sized for: every CU, or the CUs that
+// brd_set_overlap leaves to stage 1 (one workgroup per free CU, so no CU
+// runs a second round of slabs while the others idle).
+int api_apply_target() {
+    const int ov = g_ctx.overlap_cus;
+    static const char *tenv = getenv("BRD_S1_TARGET");   // tuning: workgroups per apply launch
+    if (tenv && atoi(tenv) > 0) return atoi(tenv);
+    return ov > 0 ? std::max(32, device_cus() - ov) : 256;
+}
+
+static int s2_waves() {
+    if (g_ctx.overlap_cus > 0) return g_ctx.overlap_cus;
+    static int nw = 0;
+    if (!nw) {
+        nw = std::max(64, device_cus());
+        // Bundles that can make progress at once are bounded by the chain
+        // (~one bundle lifetime / one hand-off, < 64 at N <= 16384): a smaller
+        // grid leaves CUs free for work on another stream (tuning override).
+        static const char *genv = getenv("BRD_S2_GRID");
+        if (genv && atoi(genv) > 0) nw = atoi(genv);
     }
     return nw;
 }
@@ -262,7 +287,7 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
     for (int l = 0; l < t.nlevels; ++l) {
         const double rows = (double)tree_level_rows(t, l);
         ProfScope ps("s1_apply", 4.0 * t.bk * rows * ncols, 2.0 * rows * ncols * sizeof(T), s);
-        HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, 256, fuse ? P : nullptr));
+        HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, api_apply_target(), fuse ? P : nullptr));
     }
     return BRD_OK;
 }
@@ -431,6 +456,13 @@ int brd_set_stream(void *hip_stream) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
     brd::g_ctx.user_stream = (hipStream_t)hip_stream;
     brd::g_ctx.have_user_stream = true;
+    return BRD_OK;
+}
+
+int brd_set_overlap(int s2_cus) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    if (s2_cus < 0 || s2_cus > 1024) return brd::fail(BRD_EINVAL, "brd_set_overlap: s2_cus=%d outside [0,1024]", s2_cus);
+    brd::g_ctx.overlap_cus = s2_cus;
     return BRD_OK;
 }
 

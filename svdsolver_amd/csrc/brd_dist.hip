@@ -311,7 +311,7 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
             for (int l = 0; l < tq.nlevels; ++l) {
                 const double rows = (double)tree_level_rows(tq, l);
                 void *h = api_prof_begin("s1_apply", 4.0 * bk * rows * nc, 2.0 * rows * nc * sz, s);
-                D_HIP(launch_apply<T>(false, A + (long)kb * lda + lcs, lda, tq, l, nc, ws, s, 256, Pbuf, bk));
+                D_HIP(launch_apply<T>(false, A + (long)kb * lda + lcs, lda, tq, l, nc, ws, s, api_apply_target(), Pbuf, bk));
                 api_prof_end(h, s);
             }
         }
@@ -359,7 +359,7 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
             for (int l = 0; l < tl.nlevels; ++l) {
                 const double rows = (double)tree_level_rows(tl, l);
                 void *h = api_prof_begin("s1_apply", 4.0 * bk * rows * m2, 2.0 * rows * m2 * sz, s);
-                D_HIP(launch_apply<T>(true, X, lda, tl, l, m2, ws, s));
+                D_HIP(launch_apply<T>(true, X, lda, tl, l, m2, ws, s, api_apply_target()));
                 api_prof_end(h, s);
             }
         }

@@ -70,6 +70,7 @@ hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStr
 // driver (brd_dist.hip) ------------------------------------------------------
 int api_fail(int code, const char *msg);           // sets brd_last_error, returns code
 hipStream_t api_stream();                          // the library stream
+int api_apply_target();                            // workgroups per stage-1 apply launch
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
 void api_lock();

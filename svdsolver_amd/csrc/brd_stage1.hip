@@ -820,8 +820,12 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
     const int nfac = fuse ? t.lv[level + 1].groups : 0;
     // one resident workgroup per CU (registers): aim for about one wave of
     // `target` workgroups, less the CUs the fused factor takes
+    // `target` workgroups, less the CUs the fused factor takes.  The smallest
+    // run length whose grid fits that many: a grid even one workgroup over it
+    // leaves that workgroup a second round behind a whole run of slabs.
     const int tgt = std::max(1, target - nfac);
-    const int spw = std::max(1, (groups * nslabs + tgt - 1) / tgt);
+    int spw = std::max(1, (groups * nslabs + tgt - 1) / tgt);
+    while (spw < nslabs && (long)groups * ((nslabs + spw - 1) / spw) > tgt) ++spw;
     const T *V = (const T *)ws.V[level], *VT = (const T *)ws.VT[level], *Tm = (const T *)ws.T[level];
     if (fuse) {
         dim3 grid(groups, 1 + (nslabs + spw - 1) / spw), block(kAT);

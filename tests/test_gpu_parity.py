@@ -320,3 +320,43 @@ def test_cli_svd_runs(S):
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("largest")][0]
     vals = [float(x) for x in line.split(":")[1].split()]
     assert len(vals) == 5 and all(a >= b for a, b in zip(vals, vals[1:])) and vals[0] > 0
+
+
+def test_reduce_many_pipelined_matches_serial(S):
+    """reduce_many: stage 2 of matrix i on its own stream (32 workgroups) beside
+    stage 1 of matrix i+1 (the remaining CUs).  Every matrix gets the serial
+    path's band (fp64, normwise 1e-12 on |.| of diagonals 0..b; the apply's
+    cross-wave LDS sums make bitwise equality run-dependent either way) and,
+    with the sigma geometry, the input's singular values to 1e-12 sigma_max."""
+    import torch
+    rng = np.random.default_rng(41)
+    n, b, k = 1024, 32, 4
+    As = [rng.uniform(0, 5, (n, n)) for _ in range(k)]
+    bands = []
+    for A in As:
+        dA = torch.from_numpy(A).cuda()
+        S.ge2band(dA, b)
+        bands.append(np.abs(dA.cpu().numpy()))
+    mats = [torch.from_numpy(A).cuda() for A in As]
+    got = S.reduce_many(mats, b, sigma=True)
+    i, j = np.indices((n, n))
+    inb = (j >= i) & (j - i <= b)
+    for A, (d, e) in zip(As, got):
+        sv_ref = np.linalg.svd(A, compute_uv=False)
+        sv = _sv_bidiag(d.cpu().numpy(), e.cpu().numpy())
+        assert np.max(np.abs(sv - sv_ref)) / sv_ref[0] < 1e-12
+    # stage 1 alone under the overlap setting (the remaining-CU launch sizes)
+    mats = [torch.from_numpy(A).cuda() for A in As]
+    s_a = torch.cuda.Stream()
+    S.set_overlap(S.overlap_cus(n))
+    try:
+        with torch.cuda.stream(s_a):
+            for M in mats:
+                S.ge2band(M, b, sync=False)
+        torch.cuda.synchronize()
+    finally:
+        S.set_overlap(0)
+    for M, ref_band in zip(mats, bands):
+        B = np.abs(M.cpu().numpy())
+        assert np.linalg.norm(B[inb] - ref_band[inb]) / np.linalg.norm(ref_band[inb]) < 1e-12
+        assert np.all(B[~inb] == 0)

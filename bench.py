@@ -63,6 +63,9 @@ def parse():
                         "matrix i+1 (a stream of independent reductions); off: one reduction at a time")
     p.add_argument("--s2-cus", type=int, default=None,
                    help="pipelined: CUs reserved for stage 2 (default svdsolver_amd.overlap_cus(n))")
+    p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                   help="dist mode communicator: RCCL (one GPU per rank) or the host callback over gloo "
+                        "(rehearsal of the multi-rank path with every rank on GPU 0)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the distributed path even at world size 1 (launch through torch.distributed.run)")
     return p.parse_args()
@@ -179,8 +182,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_pg = world > 1 or args.force_dist
     if use_pg:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        if args.comm == "host":   # rehearsal: several ranks may share one GPU
+            local = 0
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo", init_method="env://")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     if rank == 0 or world == 1:
         ensure_built()
@@ -201,7 +209,10 @@ def main():
     g.manual_seed(1234 + rank)
     if dist_mode:
         from svdsolver_amd import dist as D
-        D.init_rccl()
+        if args.comm == "host":
+            D.init_host()
+        else:
+            D.init_rccl()
         n_loc = D.local_cols(n, b, world, rank)
         base = torch.rand((n, max(n_loc, 1)), dtype=tdt, device=dev, generator=g)[:, :n_loc] * 5.0
         mats = [base.contiguous().clone() for _ in range(nmat)]
@@ -295,7 +306,7 @@ def main():
     # (1) the timed steps: `value` (no per-launch instrumentation inside)
     elapsed, s1, s2 = run_steps(args.warmup)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.comm == "rccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # (2) the same steps again with the library's per-launch HIP events on
@@ -329,7 +340,7 @@ def main():
                                    + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
                                       else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
                        "n": n, "band": b, "global_batch": matrices,
-                       "parallelism": (f"stage1 block-cyclic columns over {world} GPUs (RCCL), stage2 on rank "
+                       "parallelism": (f"stage1 block-cyclic columns over {world} GPUs ({'RCCL' if args.comm == 'rccl' else 'host gloo'}), stage2 on rank "
                                        + ("(matrix index mod world)" if pipelined else "0")
                                        if dist_mode else f"replicas{world}"),
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"

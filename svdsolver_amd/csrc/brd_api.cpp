@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -101,10 +102,16 @@ struct Ctx {
     bool have_user_stream = false;   // true: use user_stream (NULL = legacy default stream)
     hipStream_t user_stream = nullptr;
     hipStream_t own_stream = nullptr;
-    void *ws = nullptr;
-    size_t ws_bytes = 0;
-    int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
-    int s2_cap = 0;
+    // Device workspaces per launch stream (stage-1 tree V/T, stage-2 progress
+    // flags), so reductions on different streams can run at the same time.
+    struct Slot {
+        hipStream_t s = nullptr;
+        void *ws = nullptr;
+        size_t ws_bytes = 0;
+        int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
+        int s2_cap = 0;
+    };
+    std::deque<Slot> slots;      // deque: references stay valid as slots are added
     int *s2_err_host = nullptr;  // pinned copy of the error word
     int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
@@ -120,30 +127,45 @@ static hipStream_t stream() {
     return g_ctx.own_stream;
 }
 
-static int ensure_ws(size_t bytes) {
-    if (bytes <= g_ctx.ws_bytes) return BRD_OK;
-    if (g_ctx.ws) {
-        hipStreamSynchronize(stream());
-        hipFree(g_ctx.ws);
-        g_ctx.ws = nullptr;
-        g_ctx.ws_bytes = 0;
+static Ctx::Slot &slot() {
+    const hipStream_t s = stream();
+    for (Ctx::Slot &x : g_ctx.slots)
+        if (x.s == s) return x;
+    g_ctx.slots.emplace_back();
+    g_ctx.slots.back().s = s;
+    return g_ctx.slots.back();
+}
+
+static int ensure_ws(size_t bytes, void **out) {
+    Ctx::Slot &w = slot();
+    *out = w.ws;
+    if (bytes <= w.ws_bytes) return BRD_OK;
+    if (w.ws) {
+        hipStreamSynchronize(w.s);
+        hipFree(w.ws);
+        w.ws = nullptr;
+        w.ws_bytes = 0;
     }
-    if (hipMalloc(&g_ctx.ws, bytes) != hipSuccess)
+    if (hipMalloc(&w.ws, bytes) != hipSuccess)
         return fail(BRD_ENOMEM, "workspace allocation of %zu bytes failed", bytes);
-    g_ctx.ws_bytes = bytes;
+    w.ws_bytes = bytes;
+    *out = w.ws;
     return BRD_OK;
 }
 
-static int ensure_s2_flags(int n) {
-    if (n + 2 <= g_ctx.s2_cap) return BRD_OK;
-    if (g_ctx.s2_flags) {
-        hipStreamSynchronize(stream());
-        hipFree(g_ctx.s2_flags);
-        g_ctx.s2_flags = nullptr;
+static int ensure_s2_flags(int n, int **out) {
+    Ctx::Slot &w = slot();
+    *out = w.s2_flags;
+    if (n + 2 <= w.s2_cap) return BRD_OK;
+    if (w.s2_flags) {
+        hipStreamSynchronize(w.s);
+        hipFree(w.s2_flags);
+        w.s2_flags = nullptr;
     }
-    if (hipMalloc(&g_ctx.s2_flags, sizeof(int) * (size_t)(n + 2)) != hipSuccess)
+    if (hipMalloc(&w.s2_flags, sizeof(int) * (size_t)(n + 2)) != hipSuccess)
         return fail(BRD_ENOMEM, "stage-2 flag allocation failed");
-    g_ctx.s2_cap = n + 2;
+    w.s2_cap = n + 2;
+    *out = w.s2_flags;
     if (!g_ctx.s2_err_host && hipHostMalloc(&g_ctx.s2_err_host, sizeof(int)) != hipSuccess)
         return fail(BRD_ENOMEM, "pinned allocation failed");
     return BRD_OK;
@@ -235,9 +257,10 @@ static void prof_drain() {
 // word when the call is synchronous.
 template <typename T>
 static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sigma, bool sync, hipStream_t s) {
-    int rc = ensure_s2_flags(n);
+    int *flags = nullptr;
+    int rc = ensure_s2_flags(n, &flags);
     if (rc) return rc;
-    int *prog = g_ctx.s2_flags, *err = g_ctx.s2_flags + n + 1;
+    int *prog = flags, *err = flags + n + 1;
     {
         ProfScope ps("s2_sweep", 0, 0, s);
         HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, sigma, prog, err, s2_waves(), s));
@@ -296,7 +319,8 @@ template <typename T>
 static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
-    int rc = ensure_ws(need);
+    void *wsbase = nullptr;
+    int rc = ensure_ws(need, &wsbase);
     if (rc) return rc;
     TreeWs ws;
     for (int k = 0; k < n; k += b) {
@@ -306,14 +330,14 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
         T *P = A + (long)k * lda + k;
         // QR of the column panel A[k:m, k:k+bk], left update of A[k:m, k+bk:n]
         const Tree tq = make_tree(mp, bk);
-        tree_ws_carve(tq, sizeof(T), g_ctx.ws, ws);
+        tree_ws_carve(tq, sizeof(T), wsbase, ws);
         rc = panel_side<T>(false, P, lda, tq, ws, P + bk, n2, s);
         if (rc) return rc;
         if (n2 <= 0) continue;
         // LQ of the row panel A[k:k+bk, k+bk:n] (logical transpose), right
         // update of A[k+bk:m, k+bk:n]
         const Tree tl = make_tree(n2, bk);
-        tree_ws_carve(tl, sizeof(T), g_ctx.ws, ws);
+        tree_ws_carve(tl, sizeof(T), wsbase, ws);
         T *Q = P + bk;
         rc = panel_side<T>(true, Q, lda, tl, ws, Q + (long)bk * lda, m - k - bk, s);
         if (rc) return rc;

@@ -117,7 +117,7 @@ def test_distributed_algorithm_gloo(world, n, b, tmp_path):
 # ---------------------------------------------------------------------------
 # the library's distributed path on the GPU
 # ---------------------------------------------------------------------------
-def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path):
+def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path, root=0):
     sys.path.insert(0, os.path.dirname(HERE))
     import torch
     import torch.distributed as tdist
@@ -132,9 +132,11 @@ def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path):
     A = rng.uniform(1, 5, (n, n)).astype(dtype)
     loc = torch.from_numpy(dist.shard(A, b, world, rank)).cuda()
     dist.ge2band(loc, n, b)
-    B = dist.gather_band(loc, n, b, root=0)
-    if rank == 0:
+    B = dist.gather_band(loc, n, b, root=root)
+    if rank == root:
         np.save(out_path, B.cpu().numpy())
+    else:
+        assert B is None
     dist.finalize()
     tdist.barrier()
     tdist.destroy_process_group()
@@ -157,4 +159,20 @@ def test_distributed_stage1_gpu(world, n, b, dtype, mode, tmp_path):
     ref = S.brd_p1(A.astype(np.float64), b)
     tol = 1e-12 if dtype == np.float64 else 1e-4
     assert _band_err(band, ref, b) <= tol
+    assert np.all(band[~_band_mask(n, b)] == 0)
+
+
+@pytest.mark.gpu
+def test_distributed_gather_band_to_last_rank(tmp_path):
+    """The band gathered on a rank other than 0 (bench.py's pipelined multi-GPU
+    mode sends matrix j's band to rank j mod P): 3 ranks, root 2."""
+    import torch.multiprocessing as mp
+    import svdsolver_amd as S
+    out = str(tmp_path / "band.npy")
+    n, b = 600, 32
+    mp.spawn(_gpu_worker, args=(3, _free_port(), n, b, np.float64, "host", out, 2), nprocs=3, join=True)
+    band = np.load(out)
+    A = np.random.default_rng(5).uniform(1, 5, (n, n))
+    ref = S.brd_p1(A, b)
+    assert _band_err(band, ref, b) <= 1e-12
     assert np.all(band[~_band_mask(n, b)] == 0)

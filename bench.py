@@ -65,6 +65,8 @@ def parse():
                    help="pipelined: CUs reserved for stage 2 (default svdsolver_amd.overlap_cus(n))")
     p.add_argument("--lanes", type=int, default=1,
                    help="pipelined, one GPU: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L")
+    p.add_argument("--pad", type=int, default=0,
+                   help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                    help="dist mode communicator: RCCL (one GPU per rank) or the host callback over gloo "
                         "(rehearsal of the multi-rank path with every rank on GPU 0)")
@@ -246,7 +248,11 @@ def main():
                 s2_done[k] = e
     else:
         base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
-        mats = [base.clone() for _ in range(nmat)]
+        mats = []
+        for _ in range(nmat):
+            M = torch.empty((n, n + args.pad), dtype=tdt, device=dev)[:, :n]
+            M.copy_(base)
+            mats.append(M)
 
         def stage1(A, j):
             S.ge2band(A, b, sync=False)

@@ -138,6 +138,15 @@ def _bind_stream(x) -> None:
     lib.brd_set_stream(ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
 
 
+def _row_stride(A) -> int:
+    """Leading dimension of a row-major CUDA tensor: contiguous rows
+    (stride(1) == 1) at any row stride >= n (lda, as in the C ABI)."""
+    m, n = A.shape
+    if A.stride(1) != 1 or A.stride(0) < n:
+        raise ValueError("A must be row-major with unit column stride and row stride >= n")
+    return int(A.stride(0))
+
+
 # ---------------------------------------------------------------------------
 # stage 1
 # ---------------------------------------------------------------------------
@@ -149,10 +158,10 @@ def ge2band(A, b: int, *, sync: bool = True):
     sfx = _sfx(A.dtype)
     fn = f"brd_ge2band_{sfx}"
     if _is_torch_cuda(A):
-        assert A.is_contiguous(), "A must be contiguous"
+        lda = _row_stride(A)
         _bind_stream(A)
         flags = BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
-        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), m, n, n, int(b), 1, flags))
+        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), m, n, lda, int(b), 1, flags))
     else:
         if not (isinstance(A, np.ndarray) and A.flags.c_contiguous):
             raise TypeError("host path needs a C-contiguous numpy array")
@@ -192,7 +201,7 @@ def band2bd(A, b: int, *, exact_order: bool = False, sigma: bool = False, sync: 
         d = torch.empty(n, dtype=A.dtype, device=A.device) if extract else None
         e = torch.empty(max(n - 1, 1), dtype=A.dtype, device=A.device) if extract else None
         flags |= BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
-        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), n, n, int(b),
+        _check(fn, getattr(lib, fn)(ctypes.c_void_p(A.data_ptr()), n, _row_stride(A), int(b),
                                     ctypes.c_void_p(d.data_ptr() if extract else 0),
                                     ctypes.c_void_p(e.data_ptr() if extract else 0), flags))
         return (d, e[: n - 1]) if extract else (None, None)

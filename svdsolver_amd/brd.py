@@ -62,6 +62,15 @@ def _load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} not found: build it with `make -C svdsolver_amd` "
             "(or __graft_entry__.build()); there is no CPU fallback")
+    # torch bundles its own HIP runtime (torch/lib/libamdhip64.so, SONAME
+    # libamdhip64.so.7).  Loaded after libbrd_hip.so (which needs
+    # /opt/rocm's libamdhip64.so.7), torch would bring a second runtime that
+    # does not know the library's device pointers and vice versa; loading
+    # torch first lets the library bind to the runtime already in the process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, ci, cu = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint
     for t in ("f64", "f32"):

@@ -360,3 +360,28 @@ def test_reduce_many_pipelined_matches_serial(S):
         B = np.abs(M.cpu().numpy())
         assert np.linalg.norm(B[inb] - ref_band[inb]) / np.linalg.norm(ref_band[inb]) < 1e-12
         assert np.all(B[~inb] == 0)
+
+
+def test_padded_leading_dimension(S):
+    """Row-strided device matrices (lda = n + pad, the C ABI's lda): the band
+    and the sigma bidiagonal's singular values match the contiguous run, and
+    the padding columns are never touched."""
+    import torch
+    rng = np.random.default_rng(43)
+    n, b, pad = 640, 32, 48
+    A = rng.uniform(0, 5, (n, n))
+    ref = torch.from_numpy(A).cuda()
+    S.ge2band(ref, b)
+    P = torch.full((n, n + pad), 7.0, dtype=torch.float64, device="cuda")
+    V = P[:, :n]
+    V.copy_(torch.from_numpy(A))
+    S.ge2band(V, b)
+    i, j = np.indices((n, n))
+    inb = (j >= i) & (j - i <= b)
+    B, R = np.abs(V.cpu().numpy()), np.abs(ref.cpu().numpy())
+    assert np.linalg.norm(B[inb] - R[inb]) / np.linalg.norm(R[inb]) < 1e-12
+    assert np.all(B[~inb] == 0)
+    d, e = S.band2bd(V, b, sigma=True)
+    sv_ref = np.linalg.svd(A, compute_uv=False)
+    assert np.max(np.abs(_sv_bidiag(d.cpu().numpy(), e.cpu().numpy()) - sv_ref)) / sv_ref[0] < 1e-12
+    assert torch.all(P[:, n:] == 7.0)

@@ -63,6 +63,8 @@ def parse():
                         "matrix i+1 (a stream of independent reductions); off: one reduction at a time")
     p.add_argument("--s2-cus", type=int, default=None,
                    help="pipelined: CUs reserved for stage 2 (default svdsolver_amd.overlap_cus(n))")
+    p.add_argument("--one-at-a-time", choices=["on", "off"], default="on",
+                   help="pipelined, one GPU: also time K steps without the overlap (reported as one_at_a_time)")
     p.add_argument("--lanes", type=int, default=1,
                    help="pipelined, one GPU: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L")
     p.add_argument("--pad", type=int, default=0,
@@ -202,9 +204,12 @@ def main():
 
     n, b = args.n, args.band
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
-    nmat = args.warmup + 2 * args.steps   # warmup, the timed steps, the profiled steps
     dist_mode = (world > 1 or args.force_dist) and args.mode == "dist"
     pipelined = args.pipeline == "on"
+    serial_too = pipelined and not dist_mode and args.one_at_a_time == "on"   # also time them one at a time
+    # warmup, the timed steps, the profiled steps (+ the one-at-a-time steps)
+    nmat = args.warmup + (3 if serial_too else 2) * args.steps
+    mode = {"pipe": pipelined}
     s2_cus = S.overlap_cus(n) if pipelined else 0
     if args.s2_cus is not None:
         s2_cus = args.s2_cus
@@ -282,7 +287,7 @@ def main():
             A = mats[j]
             s_a, s_b = sa_l[j % lanes], sb_l[j % lanes]
             with torch.cuda.stream(s_a):
-                if not pipelined and last is not None:
+                if not mode["pipe"] and last is not None:
                     s_a.wait_event(last)
                 if ev:
                     ev[i][0].record(s_a)
@@ -332,6 +337,18 @@ def main():
     S.profile_enable(True)
     el_prof, _, _ = run_steps(args.warmup + args.steps)
     S.profile_enable(False)
+    one_at_a_time = None
+    if serial_too:
+        # (3) the same kind of steps without the overlap (whole chip per stage):
+        # the latency of one reduction, reported beside the stream's throughput
+        mode["pipe"] = False
+        S.set_overlap(0)
+        el_s, s1_s, s2_s = run_steps(args.warmup + 2 * args.steps)
+        S.set_overlap(s2_cus)
+        mode["pipe"] = True
+        one_at_a_time = {"value": round(args.steps * 8.0 / 3.0 * n ** 3 / el_s / 1e9, 2),
+                         "ms_per_step": round(el_s / args.steps * 1e3, 3),
+                         "stage_ms": {"stage1": round(s1_s, 3), "stage2": round(s2_s, 3)}}
     ap = S.profile_query("s1_apply")
     fa = S.profile_query("s1_factor")
     sw = S.profile_query("s2_sweep")
@@ -364,6 +381,7 @@ def main():
                                     if pipelined else "off: one reduction at a time"),
                        "stage2_cus": s2_cus or "all", "lanes": lanes},
             "latency_ms_per_reduction": round(s1 + s2, 3),
+            "one_at_a_time": one_at_a_time,
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
             "roofline": apply_roofline(ap, args.dtype),

@@ -12,6 +12,6 @@ tail -1 gpurun_out/s_$tag.log
 timeout -k 10 400 python bench.py --n $n > gpurun_out/b_$tag.log 2>&1 || { echo BENCH FAILED; tail -5 gpurun_out/b_$tag.log; exit 1; }
 grep metric gpurun_out/b_$tag.log
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 bench.py --n $n --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/p_$tag.log 2>&1 || { echo PROF FAILED; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 bench.py --n $n --steps 2 --warmup 1 --cpu-baseline off --one-at-a-time off > gpurun_out/p_$tag.log 2>&1 || { echo PROF FAILED; exit 1; }
 grep metric gpurun_out/p_$tag.log
 f=$(find gpurun_out/prof_$tag -name "*kernel_stats.csv" | head -1); echo "stats: $f"; cut -c1-160 "$f" | head -12

@@ -168,7 +168,9 @@ def stage2_roofline(sw, n, b, dtype, steps):
     P = 3 * b
     rows = sum(n - i0 for i0 in range(0, n - 1, S))
     byt = 2.0 * P * esz * rows
-    ms = sw["ms"] / max(steps, 1)
+    # per launch (one launch per reduction; in the multi-GPU pipeline rank 0
+    # runs the sweeps of only the matrices whose index is 0 mod world)
+    ms = sw["ms"] / max(sw.get("launches", steps), 1)
     traffic, src = pmc_traffic("void brd::k_band2bd_bundle<" + ("double" if dtype == "f64" else "float"))
     gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     return {"kernel": "k_band2bd_bundle (stage-2 sweeps)", "bound": "latency (dependent window chain)",

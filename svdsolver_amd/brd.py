@@ -280,8 +280,9 @@ def overlap_cus(n: int) -> int:
     (profiles/README.md, pipelined bench at n = 8192): 32 workgroups keep the
     sweep chain within 1 % of its whole-chip time and leave 224 CUs (28 per
     XCD) to stage 1 (93.7 ms beside the sweep, 88 ms alone); 64 gave 101.7 ms,
-    and 40-56 or 72-128 were slower still.  Stage 1 dominates at larger n, so
-    the reservation stays at 32."""
+    and 40-56 or 72-128 were slower still (fp32: 16 and 24 slower than 32 too;
+    the good values are multiples of 32, see profiles/README.md).  Stage 1
+    dominates at larger n, so the reservation stays at 32."""
     return 32 if n >= 1024 else 16
 
 

@@ -11,20 +11,34 @@ timed region, so no copy is timed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192] [--dtype f64] [--band 32]
 
-For N > 1 the driver launches one process per GPU (torch.distributed.run).
-Default (--mode dist): ONE N x N matrix per step, its stage 1 sharded over
-the N GPUs (block-cyclic column panels, RCCL over xGMI, brd_ge2band_dist),
-the band gathered on rank 0 and stage 2 run there (it stays single-GPU,
-BASELINE.json north_star) -- strong scaling.  --mode replicas: every rank
-reduces its own matrices (weak scaling).  The step time is the max over ranks
-and `value` is the whole-job GFLOP/s.
+N > 1: one process per GPU.  Launched by torch.distributed.run (WORLD_SIZE
+set) it joins that job; run plainly as `python bench.py --gpus N` it starts
+the N ranks itself (a torch.distributed.run child, before any GPU call) and
+exits with their status (non-zero if fewer than N GPUs are visible).
+Default (--mode dist): ONE N x N matrix per step (N = 16384, BASELINE.json
+configs[4], unless --n is given), its stage 1 sharded over the N GPUs
+(block-cyclic column panels, RCCL over xGMI, brd_ge2band_dist), the band of
+matrix j gathered on rank j mod N, which runs its stage 2 (stage 2 stays
+single-GPU, BASELINE.json north_star).  --mode replicas: every rank reduces
+its own matrices (weak scaling).  The step time is the max over ranks and
+`value` is the whole-job GFLOP/s.
+
+What `value` measures (config.value_kind): the throughput of a STREAM of
+independent reductions -- K matrices issued back to back, stage 2 of matrix
+i on its own HIP stream beside stage 1 of matrix i+1 (`--pipeline on`, the
+default).  The same K steps one reduction at a time (the reference's
+per-instance timing, timing.h:79-82) are reported as `one_at_a_time`, and
+`latency_ms_per_reduction` is one matrix's stage 1 + stage 2 under overlap.
+After every timed region the library's sticky stage-2 error words are read
+(brd_check_errors): a stalled sweep fails the run instead of being timed.
 
 Rank 0 prints ONE JSON line.  `value` comes from K timed steps with no
 per-launch instrumentation; the same K steps are then run again with the
 library's HIP events around every launch (on the stream each kernel is
 launched on) for the dominant kernel's roofline object.  Also the CPU
-baseline (the reference's own tiled algorithm, built from its sources by
-oracle/Makefile, timed on a bounded sample on this host).
+baseline: the reference's own tiled algorithm (built from its sources by
+oracle/Makefile) timed on this host at N = 320, 640, 1024 (about 10-20 s),
+with a c N^3 fit extrapolated to the GPU problem size (labelled as such).
 """
 from __future__ import annotations
 
@@ -48,11 +62,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=int, default=8192)
+    p.add_argument("--n", type=int, default=None,
+                   help="matrix size (default 8192 on one GPU, BASELINE configs[2]; 16384 across GPUs, configs[4])")
     p.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     p.add_argument("--band", type=int, default=32)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-n", type=int, default=1024)
+    p.add_argument("--cpu-n", type=str, default="320,640,1024",
+                   help="CPU-baseline sample sizes (comma separated; the largest is the reported sample)")
     p.add_argument("--s2", choices=["compat", "sigma"], default="compat",
                    help="stage-2 geometry: the reference's windows (the headline config) or the "
                         "sigma-preserving variant (BRD_SIGMA)")
@@ -83,45 +99,89 @@ def ensure_built():
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "svdsolver_amd")], check=True)
 
 
-def cpu_baseline(n: int, band: int) -> dict:
-    """Reference tiled algorithm (parallel::brd_p1 + brd_p2<double>,
-    svd_parallel.h:411/:640) on one n x n fp64 matrix, OpenMP threads =
-    min(16, cores).  Falls back to the single-threaded oracle port."""
+def host_cpus() -> dict:
+    """What this host offers the CPU baseline: the CPUs this process may run on
+    and the machine's physical core count (lscpu-equivalent from
+    /proc/cpuinfo).  On the GPU box the job's CPU share is set by
+    OMP_NUM_THREADS (16); os.cpu_count() shows the whole machine."""
+    info = {"logical_cpus": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        cores = set()
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                cores.add((phys, core))
+        if cores:
+            info["physical_cores"] = len(cores)
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
+    """The reference's tiled two-stage algorithm (parallel::brd_p1 +
+    brd_p2<double>, svd_parallel.h:411/:640), built from
+    the reference's sources by oracle/Makefile (README.md:32 flags minus
+    -march=native), on n x n fp64 matrices uniform in [0,5), b = band, at each
+    n in `sizes`.  OpenMP threads = the job's CPU share (OMP_NUM_THREADS, else
+    the affinity set).  A least-squares c n^3 fit over the samples gives the
+    EXTRAPOLATED time at the GPU problem size (not measured: ~45 min at 8192).
+    Falls back to the single-threaded C oracle (kind "port")."""
     import ctypes
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     from splitmix import uniform_matrix
-    A = uniform_matrix(n, seed=n, lo=0.0, hi=5.0, dtype=np.float64)
-    cores = min(16, os.cpu_count() or 1)
+    hc = host_cpus()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hc.get("affinity_cpus") or hc["logical_cpus"] or 1
     ref = os.path.join(REPO, "oracle", "_ref", "libref_fast.so")
+    L = None
     if os.path.exists(ref):
         L = ctypes.CDLL(ref)
-        L.ref_set_threads(cores)
-        B = A.copy()
-        t0 = time.perf_counter()
-        L.ref_brd_p1_f64(B.ctypes.data_as(ctypes.c_void_p), n, band)
-        L.ref_brd_p2_f64(B.ctypes.data_as(ctypes.c_void_p), n, band)
-        dt = time.perf_counter() - t0
-        kind, used = "reference", cores
+        L.ref_set_threads(threads)
+        kind, used = "reference", threads
     else:
         from oracle import oracle
-        t0 = time.perf_counter()
-        B = oracle.brd_p1(A, band)
-        oracle.brd_p2(B, band)
-        dt = time.perf_counter() - t0
         kind, used = "port", 1
-    return {"value": round(8.0 / 3.0 * n ** 3 / dt / 1e9, 4), "unit": "GFLOP/s", "cores": used,
-            "kind": kind, "sample": f"one {n}x{n} fp64 two-stage reduction, b={band}, {dt:.2f} s"}
+    pts = []
+    for n in sizes:
+        A = uniform_matrix(n, seed=n, lo=0.0, hi=5.0, dtype=np.float64)
+        t0 = time.perf_counter()
+        if L is not None:
+            L.ref_brd_p1_f64(A.ctypes.data_as(ctypes.c_void_p), n, band)
+            L.ref_brd_p2_f64(A.ctypes.data_as(ctypes.c_void_p), n, band)
+        else:
+            oracle.brd_p2(oracle.brd_p1(A, band), band)
+        pts.append((n, time.perf_counter() - t0))
+    n_s, dt = pts[-1]
+    c = sum(t * n ** 3 for n, t in pts) / sum(float(n) ** 6 for n, _ in pts)   # least squares t = c n^3
+    t_ext = c * float(gpu_n) ** 3
+    return {"value": round(8.0 / 3.0 * n_s ** 3 / dt / 1e9, 4), "unit": "GFLOP/s", "cores": used,
+            "kind": kind, "sample": f"{n_s}x{n_s} fp64 two-stage reduction, b={band}, {dt:.2f} s, "
+                                    f"{used} OpenMP threads",
+            "threads": used, "host": hc,
+            "sizes_s": {str(n): round(t, 3) for n, t in pts},
+            "extrapolated": {"n": gpu_n, "seconds": round(t_ext, 1),
+                             "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_ext / 1e9, 4),
+                             "basis": "least-squares c*n^3 over the sampled sizes; NOT measured"}}
 
 
-def pmc_traffic(*kernel_prefixes: str):
+def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
-    (tools/pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled
-    for gfx950's 64-B tally of 128-B requests, MI355X_MICROARCH.md 'HBM').  The
-    counters cannot be read inside this process, so the profile of the same
-    command is the source; None when absent."""
+    of THIS configuration, profiles/r*_pmc_n{n}_{dtype}.txt (tools/pmc.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes over the same bench command;
+    FETCH_SIZE doubled for gfx950's 64-B tally of 128-B requests,
+    MI355X_MICROARCH.md 'HBM').  The counters cannot be read inside this
+    process, so the profile of the same command is the source; None when no
+    summary of this configuration is committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.txt")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_n{n}_{dtype}.txt")))
     if not files:
         return None, None
     tot, cnt = 0.0, 0
@@ -137,7 +197,7 @@ def pmc_traffic(*kernel_prefixes: str):
     return (tot / cnt if cnt else None), os.path.relpath(files[-1], REPO)
 
 
-def apply_roofline(ap, dtype):
+def apply_roofline(ap, dtype, n):
     """Stage-1 trailing update (k_apply, and k_apply_factor: the same apply with
     the next tree level's factor in one extra workgroup): per element of the
     trailing matrix one read + one write against 4b flops -> 8 flop/B at b = 32
@@ -146,7 +206,7 @@ def apply_roofline(ap, dtype):
     gbs = ap["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tf = ap["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     tn = "double" if dtype == "f64" else "float"
-    traffic, src = pmc_traffic("void brd::k_apply<" + tn, "void brd::k_apply_factor<" + tn)
+    traffic, src = pmc_traffic(n, dtype, "void brd::k_apply<" + tn, "void brd::k_apply_factor<" + tn)
     return {"kernel": "k_apply + k_apply_factor (stage-1 trailing update, MFMA)", "bound": "hbm",
             "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,
@@ -166,22 +226,62 @@ def stage2_roofline(sw, n, b, dtype, steps):
     esz = 8 if dtype == "f64" else 4
     S = 3 if dtype == "f64" else 5      # sweeps per bundle (brd_stage2.hip bundle_plan)
     P = 3 * b
+    # minimum: the band (3b stored diagonals per row: the fill of a bulge
+    # reaches b-1 below and 2b-1 above the diagonal) read once, written once
+    minimum = 2.0 * n * P * esz
+    # the design's volume: every bundle of S sweeps streams the rows below its
+    # first sweep in and out of its LDS ring once
     rows = sum(n - i0 for i0 in range(0, n - 1, S))
-    byt = 2.0 * P * esz * rows
+    streamed = 2.0 * P * esz * rows
     # per launch (one launch per reduction; in the multi-GPU pipeline rank 0
     # runs the sweeps of only the matrices whose index is 0 mod world)
     ms = sw["ms"] / max(sw.get("launches", steps), 1)
-    traffic, src = pmc_traffic("void brd::k_band2bd_bundle<" + ("double" if dtype == "f64" else "float"))
-    gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    traffic, src = pmc_traffic(n, dtype, "void brd::k_band2bd_bundle<" + ("double" if dtype == "f64" else "float"))
     return {"kernel": "k_band2bd_bundle (stage-2 sweeps)", "bound": "latency (dependent window chain)",
-            "ms": round(ms, 3), "hbm_gbs_algorithmic": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
-            "algorithmic_bytes_per_launch": round(byt), "traffic": round(traffic) if traffic else None,
-            "traffic_source": src, "windows": n * ((n // b) * 2),
-            "us_per_sweep": round(ms * 1e3 / max(n - 1, 1), 3)}
+            "ms": round(ms, 3),
+            "minimum_bytes": round(minimum), "streamed_bytes_by_design": round(streamed),
+            "traffic": round(traffic) if traffic else None, "traffic_source": src,
+            "traffic_over_minimum": round(traffic / minimum, 1) if traffic else None,
+            "hbm_gbs_streamed": round(streamed / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
+            "windows": n * ((n // b) * 2),
+            "us_per_sweep": round(ms * 1e3 / max(n - 1, 1), 3),
+            "chain_bound_note": "about 4 dependent windows per sweep (lag-3 rule, DESIGN.md Stage 2)"}
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def maybe_spawn(args) -> None:
+    """`python bench.py --gpus N` with no launcher around it: start the N ranks
+    as a torch.distributed.run child (one process per GPU, rendezvous on
+    127.0.0.1) and exit with its status.  Runs before this process touches
+    the GPU (torch.cuda.device_count() does not initialise it on this image),
+    so nothing here is exec'd from a GPU-initialised process."""
+    if "WORLD_SIZE" in os.environ:
+        w = int(os.environ["WORLD_SIZE"])
+        if args.gpus != 1 and args.gpus != w:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={w}")
+        return
+    if args.gpus <= 1:
+        return
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} requested but only {ndev} GPU(s) are visible")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def main():
     args = parse()
+    maybe_spawn(args)
     import torch
     import torch.distributed as dist
 
@@ -205,6 +305,8 @@ def main():
     import svdsolver_amd as S
 
     n, b = args.n, args.band
+    if n is None:
+        n = 8192 if world == 1 else 16384   # BASELINE.json configs[2] / configs[4]
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     dist_mode = (world > 1 or args.force_dist) and args.mode == "dist"
     pipelined = args.pipeline == "on"
@@ -308,6 +410,7 @@ def main():
 
     issue(0, args.warmup)
     torch.cuda.synchronize(dev)
+    S.check_errors()
 
     def run_steps(first):
         """K steps bracketed by barrier + synchronize; per-step stage split by
@@ -323,6 +426,9 @@ def main():
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        # a stage-2 sweep that gave up waiting (sticky error word) fails the
+        # run rather than being timed as a valid reduction
+        S.check_errors()
         s2 = [e[1].elapsed_time(e[2][1]) for i, e in enumerate(ev) if not dist_mode or rank == root_of(first + i)]
         return (el, sum(e[0].elapsed_time(e[2][0]) for e in ev) / args.steps,
                 sum(s2) / max(1, len(s2)))
@@ -372,21 +478,28 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic uniform [0,5) N x N, resident in HBM",
-            "config": {"workload": f"two-stage bidiagonal reduction {n}x{n} {args.dtype}, band {b}, "
+            "config": {"workload": (f"stream of independent two-stage bidiagonal reductions {n}x{n} {args.dtype}"
+                                    if pipelined else f"two-stage bidiagonal reduction {n}x{n} {args.dtype}, one at a time")
+                                   + f", band {b}, "
                                    + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
                                       else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
+                       "value_kind": ("stream throughput: K matrices back to back, stage 2 of matrix i beside stage 1 "
+                                      "of matrix i+1 (per-reduction latency: latency_ms_per_reduction; one reduction "
+                                      "at a time: one_at_a_time)" if pipelined else "one reduction at a time"),
                        "n": n, "band": b, "global_batch": matrices,
+                       "matrices_per_timed_region": matrices * args.steps,
                        "parallelism": (f"stage1 block-cyclic columns over {world} GPUs ({'RCCL' if args.comm == 'rccl' else 'host gloo'}), stage2 on rank "
                                        + ("(matrix index mod world)" if pipelined else "0")
                                        if dist_mode else f"replicas{world}"),
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
                                     if pipelined else "off: one reduction at a time"),
-                       "stage2_cus": s2_cus or "all", "lanes": lanes},
+                       "stage2_cus": s2_cus or "all", "lanes": lanes,
+                       "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},
             "latency_ms_per_reduction": round(s1 + s2, 3),
             "one_at_a_time": one_at_a_time,
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
-            "roofline": apply_roofline(ap, args.dtype),
+            "roofline": apply_roofline(ap, args.dtype, n),
             "stage2": stage2_roofline(sw, n, b, args.dtype, args.steps),
             "kernel_ms_per_step": {"s1_apply": round(ap["ms"] / args.steps, 3),
                                    "s1_factor": round(fa["ms"] / args.steps, 3),
@@ -394,7 +507,7 @@ def main():
         }
         if args.cpu_baseline == "auto":
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_n, b)
+                out["cpu_baseline"] = cpu_baseline([int(x) for x in args.cpu_n.split(",")], b, n)
             except Exception as e:   # the baseline is reported, never required
                 out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
         print(json.dumps(out), flush=True)

@@ -87,7 +87,15 @@ int brd_use_own_stream(void);
  * remaining CUs; 0 restores the defaults (each stage on the whole chip).
  * No reference counterpart (the reference runs one reduction at a time,
  * svd_cuda_2.cu:1387 / timing.h:55). */
-int brd_set_overlap(int s2_cus);
+int brd_set_overlap(int s2_cus);   /* 0 <= s2_cus < device CUs, else BRD_EINVAL */
+
+/* Drains every stream the library has launched on and reports failures of
+ * asynchronous (BRD_ASYNC) calls: a stage-2 sweep whose bounded spin gave up
+ * (its output is then invalid) or a pending HIP error.  The stage-2 error
+ * word of a stream is sticky: no launch resets it; a synchronous band2bd on
+ * that stream or this call reads and clears it.  Call it after a batch of
+ * asynchronous work before trusting the results. */
+int brd_check_errors(void);
 
 /* Per-kernel device timing for roofline reporting.  While enabled, the library
  * brackets every launch of the named kernel class with HIP events on the

@@ -37,7 +37,7 @@ BRD_SIGMA = 0x10
 
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
-    "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
+    "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_check_errors", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
     "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
     "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_last_error", "brd_version",
@@ -89,6 +89,8 @@ def _load() -> ctypes.CDLL:
     L.brd_use_own_stream.restype = ci
     L.brd_set_overlap.argtypes = [ci]
     L.brd_set_overlap.restype = ci
+    L.brd_check_errors.argtypes = []
+    L.brd_check_errors.restype = ci
     L.brd_profile_enable.argtypes = [ci]
     L.brd_profile_enable.restype = ci
     L.brd_profile_reset.argtypes = []
@@ -317,7 +319,15 @@ def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = No
     torch.cuda.current_stream(dev).wait_stream(s_b)
     if sync:
         torch.cuda.synchronize(dev)
+        check_errors()
     return out
+
+
+def check_errors() -> None:
+    """brd_check_errors (include/brd.h): drain the library's streams and raise
+    :class:`BrdError` if an asynchronous stage-2 sweep hit its spin limit (its
+    output is invalid) or a HIP error is pending."""
+    _check("brd_check_errors", lib.brd_check_errors())
 
 
 # ---------------------------------------------------------------------------

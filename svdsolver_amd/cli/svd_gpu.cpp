@@ -11,8 +11,12 @@
 //       reduction there and never matches them).
 //   svd_gpu benchmark <step> <nsteps> <ninst> <b> [--dtype f32|f64] [--csv PATH]
 //       N = k*step for k = 1..nsteps, ninst matrices uniform in [0,5) each;
-//       prints "N = <n> | <sec> sec" per size and writes the reference's 2-row
-//       CSV (N row, stage-1 seconds row) plus a third row with stage-2 seconds.
+//       prints "N = <n> | <sec> sec" per size (the reference times the band
+//       reduction, svd_cuda_2.cu:1397) and writes the reference's 2-line CSV
+//       (svd_cuda_2.cu:1407-1426: the N values, then the stage-1 seconds, ", "
+//       separated, no trailing newline) for its plotting notebook.  Stage 2 is
+//       timed too: printed on the same line and written in the same 2-line
+//       format to <csv stem>_stage2.csv.
 //   svd_gpu svd <N> [--dtype f32|f64] [--band B]
 //       Singular values of an N x N matrix uniform in [0,5): stage 1, stage 2 with
 //       the sigma-preserving geometry (BRD_SIGMA) and the host bidiagonal QR
@@ -23,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <filesystem>
 #include <fstream>
 #include <string>
 #include <vector>
@@ -84,6 +89,22 @@ int check(int n, const std::string &dir, const char *tname) {
     return 0;
 }
 
+// The reference's result file (svd_cuda_2.cu:1407-1426): line 1 the sizes,
+// line 2 the seconds, ", " between values, no newline after the last line.
+bool write_csv(const std::string &path, const std::vector<int> &xs, const std::vector<double> &ys) {
+    const std::filesystem::path parent = std::filesystem::path(path).parent_path();
+    std::error_code ec;
+    if (!parent.empty()) std::filesystem::create_directories(parent, ec);
+    std::ofstream f(path);
+    if (!f) {
+        std::fprintf(stderr, "cannot write %s\n", path.c_str());
+        return false;
+    }
+    for (size_t i = 0; i < xs.size(); ++i) f << xs[i] << (i + 1 < xs.size() ? ", " : "\n");
+    for (size_t i = 0; i < ys.size(); ++i) f << (float)ys[i] << (i + 1 < ys.size() ? ", " : "");
+    return (bool)f;
+}
+
 template <typename T>
 int benchmark(int step, int nsteps, int ninst, int b, const std::string &csv) {
     std::printf("Benchmark: MI355X two-stage bidiagonal reduction (%s)\n", sizeof(T) == 8 ? "fp64" : "fp32");
@@ -111,17 +132,19 @@ int benchmark(int step, int nsteps, int ninst, int b, const std::string &csv) {
         t1 /= ninst;
         t2 /= ninst;
         const double gf = 8.0 / 3.0 * (double)n * n * n / (t1 + t2) / 1e9;
-        std::printf("N = %d | %g sec (dense -> band) | %g sec (band -> bidiagonal) | %.2f GFLOP/s (host buffers, "
+        std::printf("N = %d | %g sec | band -> bidiagonal %g sec | %.2f GFLOP/s two-stage (host buffers, "
                     "PCIe included)\n", n, t1, t2, gf);
         xs.push_back(n);
         y1.push_back(t1);
         y2.push_back(t2);
     }
-    std::ofstream f(csv);
-    for (size_t i = 0; i < xs.size(); ++i) f << xs[i] << (i + 1 < xs.size() ? ", " : "\n");
-    for (size_t i = 0; i < y1.size(); ++i) f << y1[i] << (i + 1 < y1.size() ? ", " : "\n");
-    for (size_t i = 0; i < y2.size(); ++i) f << y2[i] << (i + 1 < y2.size() ? ", " : "\n");
     std::printf("Writing results to file ... %s\n", csv.c_str());
+    if (!write_csv(csv, xs, y1)) return 1;
+    const size_t dot = csv.rfind('.');
+    const std::string csv2 = (dot == std::string::npos || dot < csv.rfind('/') + 1 ? csv : csv.substr(0, dot)) +
+                             "_stage2.csv";
+    if (!write_csv(csv2, xs, y2)) return 1;
+    std::printf("Done.\n");
     return 0;
 }
 

@@ -108,11 +108,17 @@ struct Ctx {
         hipStream_t s = nullptr;
         void *ws = nullptr;
         size_t ws_bytes = 0;
-        int *s2_flags = nullptr;     // stage-2 progress flags (n+1) + error word
+        int *s2_flags = nullptr;     // stage-2 progress flags (n+1)
         int s2_cap = 0;
+        // Stage-2 error word: written by the sweep kernel when a bounded spin
+        // gives up, never reset by a launch (an asynchronous call's failure
+        // stays visible until a synchronous call or brd_check_errors reads it).
+        int *s2_err = nullptr;
+        void *stage = nullptr;       // host-pointer calls: cached HBM staging buffer
+        size_t stage_bytes = 0;
     };
     std::deque<Slot> slots;      // deque: references stay valid as slots are added
-    int *s2_err_host = nullptr;  // pinned copy of the error word
+    int *s2_err_host = nullptr;  // pinned copy of an error word
     int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
     std::map<std::string, ProfAcc> acc;
@@ -153,21 +159,60 @@ static int ensure_ws(size_t bytes, void **out) {
     return BRD_OK;
 }
 
-static int ensure_s2_flags(int n, int **out) {
+static int ensure_s2_flags(int n, int **out, int **err) {
     Ctx::Slot &w = slot();
+    if (!g_ctx.s2_err_host && hipHostMalloc(&g_ctx.s2_err_host, sizeof(int)) != hipSuccess)
+        return fail(BRD_ENOMEM, "pinned allocation failed");
+    if (!w.s2_err) {
+        if (hipMalloc(&w.s2_err, sizeof(int)) != hipSuccess) return fail(BRD_ENOMEM, "stage-2 error word allocation failed");
+        if (hipMemsetAsync(w.s2_err, 0, sizeof(int), w.s) != hipSuccess) return fail(BRD_EHIP, "stage-2 error word reset failed");
+    }
+    *err = w.s2_err;
     *out = w.s2_flags;
     if (n + 2 <= w.s2_cap) return BRD_OK;
     if (w.s2_flags) {
         hipStreamSynchronize(w.s);
         hipFree(w.s2_flags);
         w.s2_flags = nullptr;
+        w.s2_cap = 0;
     }
     if (hipMalloc(&w.s2_flags, sizeof(int) * (size_t)(n + 2)) != hipSuccess)
         return fail(BRD_ENOMEM, "stage-2 flag allocation failed");
     w.s2_cap = n + 2;
     *out = w.s2_flags;
-    if (!g_ctx.s2_err_host && hipHostMalloc(&g_ctx.s2_err_host, sizeof(int)) != hipSuccess)
-        return fail(BRD_ENOMEM, "pinned allocation failed");
+    return BRD_OK;
+}
+
+// Reads (and clears) a slot's stage-2 error word; the slot's stream is drained.
+static int take_s2_error(Ctx::Slot &w, int *code) {
+    *code = 0;
+    if (!w.s2_err) return BRD_OK;
+    HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, w.s2_err, sizeof(int), hipMemcpyDeviceToHost, w.s));
+    HIP_TRY(hipStreamSynchronize(w.s));
+    *code = *g_ctx.s2_err_host;
+    if (*code) {
+        HIP_TRY(hipMemsetAsync(w.s2_err, 0, sizeof(int), w.s));
+        HIP_TRY(hipStreamSynchronize(w.s));
+    }
+    return BRD_OK;
+}
+
+// HBM staging buffer of the host-pointer paths, cached per launch stream (no
+// allocation per call, nothing to free on an error return).
+static int ensure_stage(size_t bytes, void **out) {
+    Ctx::Slot &w = slot();
+    if (bytes > w.stage_bytes) {
+        if (w.stage) {
+            hipStreamSynchronize(w.s);
+            hipFree(w.stage);
+            w.stage = nullptr;
+            w.stage_bytes = 0;
+        }
+        if (hipMalloc(&w.stage, bytes) != hipSuccess)
+            return fail(BRD_ENOMEM, "device staging allocation of %zu bytes failed", bytes);
+        w.stage_bytes = bytes;
+    }
+    *out = w.stage;
     return BRD_OK;
 }
 
@@ -196,7 +241,7 @@ static int s2_waves() {
     if (g_ctx.overlap_cus > 0) return g_ctx.overlap_cus;
     static int nw = 0;
     if (!nw) {
-        nw = std::max(64, device_cus());
+        nw = device_cus();   // launch_band2bd clamps to the co-resident capacity
         // Bundles that can make progress at once are bounded by the chain
         // (~one bundle lifetime / one hand-off, < 64 at N <= 16384): a smaller
         // grid leaves CUs free for work on another stream (tuning override).
@@ -253,22 +298,25 @@ static void prof_drain() {
     g_ctx.pending.clear();
 }
 
-// Runs the stage-2 sweep on a device matrix; checks the kernel's spin-limit
-// word when the call is synchronous.
+// Runs the stage-2 sweep on a device matrix.  A synchronous call checks (and
+// clears) the slot's sticky spin-limit word; asynchronous calls leave it for
+// the next synchronous call or brd_check_errors().
 template <typename T>
 static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sigma, bool sync, hipStream_t s) {
-    int *flags = nullptr;
-    int rc = ensure_s2_flags(n, &flags);
+    int *prog = nullptr, *err = nullptr;
+    int rc = ensure_s2_flags(n, &prog, &err);
     if (rc) return rc;
-    int *prog = flags, *err = flags + n + 1;
     {
         ProfScope ps("s2_sweep", 0, 0, s);
         HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, sigma, prog, err, s2_waves(), s));
     }
     if (sync) {
-        HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, err, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (*g_ctx.s2_err_host) return fail(BRD_EHIP, "stage-2 pipeline stalled (spin limit hit)");
+        int code = 0;
+        rc = take_s2_error(slot(), &code);
+        if (rc) return rc;
+        if (code)
+            return fail(BRD_EHIP, "stage-2 pipeline stalled (spin limit hit, code %d) in this or an earlier "
+                                  "asynchronous call on this stream", code);
     }
     return BRD_OK;
 }
@@ -394,17 +442,17 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
         rc = ge2band_device<T>(A, m, n, lda, b, s);
         if (rc == BRD_OK && !(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
     } else {
-        T *d = nullptr;
-        if (hipMalloc(&d, sizeof(T) * (size_t)m * n) != hipSuccess)
-            return fail(BRD_ENOMEM, "device matrix allocation failed");
+        void *stage = nullptr;
+        rc = ensure_stage(sizeof(T) * (size_t)m * n, &stage);
+        if (rc) return rc;
+        T *d = (T *)stage;
         HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, m,
                                  hipMemcpyHostToDevice, s));
         rc = ge2band_device<T>(d, m, n, n, b, s);
         if (rc == BRD_OK)
             HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, m,
                                      hipMemcpyDeviceToHost, s));
-        hipStreamSynchronize(s);
-        hipFree(d);
+        HIP_TRY(hipStreamSynchronize(s));
     }
     if (rc == BRD_OK) {
         hipError_t e = hipGetLastError();
@@ -433,14 +481,14 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
         if (extract) HIP_TRY(launch_extract_bidiag<T>(A, n, lda, dd, ee, s));
         if (!(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
     } else {
-        T *d = nullptr, *de = nullptr;
-        if (hipMalloc(&d, sizeof(T) * ((size_t)n * n + 2 * (size_t)n)) != hipSuccess)
-            return fail(BRD_ENOMEM, "device matrix allocation failed");
-        de = d + (size_t)n * n;
+        void *stage = nullptr;
+        int rc = ensure_stage(sizeof(T) * ((size_t)n * n + 2 * (size_t)n), &stage);
+        if (rc) return rc;
+        T *d = (T *)stage, *de = d + (size_t)n * n;
         HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, n,
                                  hipMemcpyHostToDevice, s));
-        int rc = band2bd_device<T>(d, n, n, b, exact, sigma, true, s);
-        if (rc) { hipFree(d); return rc; }
+        rc = band2bd_device<T>(d, n, n, b, exact, sigma, true, s);
+        if (rc) return rc;
         HIP_TRY(launch_extract_bidiag<T>(d, n, n, de, de + n, s));
         HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, n,
                                  hipMemcpyDeviceToHost, s));
@@ -448,8 +496,7 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
             HIP_TRY(hipMemcpyAsync(dd, de, sizeof(T) * n, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipMemcpyAsync(ee, de + n, sizeof(T) * (n - 1), hipMemcpyDeviceToHost, s));
         }
-        hipStreamSynchronize(s);
-        hipFree(d);
+        HIP_TRY(hipStreamSynchronize(s));
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(BRD_EHIP, "stage 2: %s", hipGetErrorString(e));
@@ -485,8 +532,27 @@ int brd_set_stream(void *hip_stream) {
 
 int brd_set_overlap(int s2_cus) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
-    if (s2_cus < 0 || s2_cus > 1024) return brd::fail(BRD_EINVAL, "brd_set_overlap: s2_cus=%d outside [0,1024]", s2_cus);
+    const int cus = brd::device_cus();
+    if (s2_cus < 0 || s2_cus >= cus)
+        return brd::fail(BRD_EINVAL, "brd_set_overlap: s2_cus=%d outside [0,%d) (device CUs)", s2_cus, cus);
     brd::g_ctx.overlap_cus = s2_cus;
+    return BRD_OK;
+}
+
+int brd_check_errors(void) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    std::string bad;
+    for (brd::Ctx::Slot &w : brd::g_ctx.slots) {
+        int code = 0;
+        const int rc = brd::take_s2_error(w, &code);
+        if (rc) return rc;
+        if (code) bad += (bad.empty() ? "" : ", ") + std::to_string(code);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return brd::fail(BRD_EHIP, "HIP error: %s", hipGetErrorString(e));
+    if (!bad.empty())
+        return brd::fail(BRD_EHIP, "stage-2 pipeline stalled in an asynchronous call (spin limit hit, code %s)",
+                         bad.c_str());
     return BRD_OK;
 }
 

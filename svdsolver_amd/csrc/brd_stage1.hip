@@ -614,6 +614,7 @@ __device__ __forceinline__ void slab_store(T *base, long ld, const int *sMap, in
 template <typename T>
 struct ApplyLds {
     T sX[kASlab * kPT];
+    T sWp[kAW][32 * 16];   // per-wave partials of W = V^T X, summed in wave order (deterministic)
     T sW[32 * 17];
     T sW2[32 * 17];
     T sT[32 * 32];
@@ -627,7 +628,9 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
                                            const T *__restrict__ VTws, const T *__restrict__ Tws)
 {
     typedef typename Mfma<T>::v4 v4;
+    static_assert(kAT == 32 * 16, "one thread per element of W in the cross-wave sum");
     auto &sX = L.sX;
+    auto &sWp = L.sWp;
     auto &sW = L.sW;
     auto &sW2 = L.sW2;
     auto &sT = L.sT;
@@ -649,7 +652,6 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
 
     if (tid < nr) sMap[tid] = group_row(tid, grp, la);
     for (int e = tid; e < 32 * 32; e += kAT) sT[e] = Tm[e];
-    for (int e = tid; e < 32 * 17; e += kAT) sW[e] = (T)0;
 
     // ---- V fragments for this wave's row blocks (registers, whole run) -----
     T Vw[kAB][4][2];   // W phase, A operand of V^T: V[blk*16 + q + 4s][ab*16 + arow]
@@ -696,8 +698,17 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
 #pragma unroll
                 for (int ab = 0; ab < 2; ++ab)
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) atomicAdd(&sW[(ab * 16 + q + 4 * g) * 17 + l15], acc[ab][g]);
+                    for (int g = 0; g < 4; ++g) sWp[w][(ab * 16 + q + 4 * g) * 16 + l15] = acc[ab][g];
             }
+        }
+        lds_barrier();
+        // cross-wave sum in wave order: the result does not depend on which
+        // wave finishes first (stage 1 is bitwise reproducible run to run)
+        {
+            const int nwp = min(kAW, nblk);
+            T s = sWp[0][tid];
+            for (int k = 1; k < nwp; ++k) s += sWp[k][tid];
+            sW[(tid >> 4) * 17 + (tid & 15)] = s;
         }
         lds_barrier();
         // ---- W2 = -(T^T W) -------------------------------------------------
@@ -713,7 +724,6 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
             for (int g = 0; g < 4; ++g) sW2[(ab * 16 + q + 4 * g) * 17 + l15] = -acc[g];
         }
         lds_barrier();
-        for (int e = tid; e < 32 * 17; e += kAT) sW[e] = (T)0;   // ready for the next slab
         // ---- X += V W2 ----------------------------------------------------
         {
             T bw[8];

@@ -1148,14 +1148,25 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
     return false;
 }
 
-// prog: n+1 ints, err: 1 int (device workspace, zeroed here).
+// Workgroups of `fn` (block threads, dynamic LDS bytes) that can be resident
+// at once on the device: the persistent sweep kernels hand bundles / sweeps
+// round-robin and wait on their predecessors, so every workgroup of the grid
+// must be able to run at the same time.
+static int coresident_limit(const void *fn, int threads, size_t lds) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess) return 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return per_cu * cus;
+}
+
+// prog: n+1 ints (zeroed here); err: the caller's sticky error word (never
+// reset here: a nonzero value from an earlier launch stays visible).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,
                           int nwaves, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(prog, 0, sizeof(int) * (size_t)(n + 1), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     const int sg = sigma_geom ? 1 : 0;
     static const char *sel = getenv("BRD_S2_SCHEDULE");   // "pipe" selects the HBM-only schedule
@@ -1169,7 +1180,6 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
                                 : bundle_plan<T, false, 1>(n, b, S, R);
     if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule
         const int nbundles = (n - 1 + S - 1) / S;
-        const int grid = std::max(1, std::min(nwaves, nbundles));
         const dim3 block(64 * (W * S + 3));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
         const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0, 1>
@@ -1179,6 +1189,9 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
+        const int cap = coresident_limit(fn, (int)block.x, lds);
+        if (cap < 1) return hipErrorInvalidConfiguration;
+        const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
         if (exact_order)
             hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 2)
@@ -1189,7 +1202,10 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
             hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
-    const int grid = std::max(1, std::min(nwaves, n - 1));
+    const void *pfn = exact_order ? (const void *)k_band2bd_pipe<T, true> : (const void *)k_band2bd_pipe<T, false>;
+    const int cap = coresident_limit(pfn, 64, 0);
+    if (cap < 1) return hipErrorInvalidConfiguration;
+    const int grid = std::max(1, std::min(std::min(nwaves, cap), n - 1));
     if (exact_order)
         hipLaunchKernelGGL((k_band2bd_pipe<T, true>), dim3(grid), dim3(64), 0, s, A, n, n, lda, b, sg, prog, err);
     else

@@ -24,7 +24,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from .brd import (BRD_ASYNC, BRD_DEVICE_PTR, COLL_FN, _bind_stream, _check, _sfx, lib)
+from .brd import (BRD_ASYNC, BRD_DEVICE_PTR, COLL_FN, _bind_stream, _check, _row_stride, _sfx, lib)
 
 COLL_BCAST, COLL_ALLGATHER, COLL_ALLREDUCE_SUM = 0, 1, 2
 DT_BYTE, DT_F32, DT_F64 = 0, 1, 2
@@ -153,6 +153,16 @@ def finalize() -> None:
 # ---------------------------------------------------------------------------
 # compute
 # ---------------------------------------------------------------------------
+def _local_ld(A_loc) -> int:
+    """Leading dimension of a shard: its row stride (row-major, unit column
+    stride), or 1 for an empty shard (n_loc == 0 on ranks without panels)."""
+    if A_loc.dim() != 2:
+        raise ValueError("A_loc must be a 2-D m x n_loc tensor")
+    if A_loc.numel() == 0:
+        return 1
+    return _row_stride(A_loc)
+
+
 def ge2band(A_loc, n: int, b: int, *, sync: bool = True):
     """Distributed dense -> band IN PLACE on this rank's shard ``A_loc``
     (torch CUDA tensor, m x n_loc, contiguous; n_loc may be 0).  Every rank
@@ -160,7 +170,7 @@ def ge2band(A_loc, n: int, b: int, *, sync: bool = True):
     m = A_loc.shape[0]
     sfx = _sfx(A_loc.dtype)
     _bind_stream(A_loc)
-    ld = max(1, A_loc.shape[1])
+    ld = _local_ld(A_loc)
     ptr = A_loc.data_ptr() if A_loc.numel() else 0
     flags = BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
     fn = f"brd_ge2band_dist_{sfx}"
@@ -179,12 +189,16 @@ def gather_band(A_loc, n: int, b: int, root: int = 0, *, out=None, sync: bool = 
     _bind_stream(A_loc)
     me = dist.get_rank()
     B: Optional[torch.Tensor] = None
+    ldb = int(n)
     if me == root:
         B = out if out is not None else torch.empty((m, n), dtype=A_loc.dtype, device=A_loc.device)
-    ld = max(1, A_loc.shape[1])
+        if tuple(B.shape) != (m, n) or B.dtype != A_loc.dtype:
+            raise ValueError(f"out must be a {m} x {n} tensor of {A_loc.dtype}")
+        ldb = _row_stride(B)
+    ld = _local_ld(A_loc)
     ptr = A_loc.data_ptr() if A_loc.numel() else 0
     flags = BRD_DEVICE_PTR | (0 if sync else BRD_ASYNC)
     fn = f"brd_dist_gather_band_{sfx}"
     _check(fn, getattr(lib, fn)(ctypes.c_void_p(ptr), m, int(n), ld, int(b),
-                                ctypes.c_void_p(B.data_ptr() if B is not None else 0), int(n), int(root), flags))
+                                ctypes.c_void_p(B.data_ptr() if B is not None else 0), ldb, int(root), flags))
     return B

@@ -325,8 +325,8 @@ def test_cli_svd_runs(S):
 def test_reduce_many_pipelined_matches_serial(S):
     """reduce_many: stage 2 of matrix i on its own stream (32 workgroups) beside
     stage 1 of matrix i+1 (the remaining CUs).  Every matrix gets the serial
-    path's band (fp64, normwise 1e-12 on |.| of diagonals 0..b; the apply's
-    cross-wave LDS sums make bitwise equality run-dependent either way) and,
+    path's band bit for bit (the launch sizing under the overlap changes which
+    workgroup runs which slabs, never the per-element arithmetic order) and,
     with the sigma geometry, the input's singular values to 1e-12 sigma_max."""
     import torch
     rng = np.random.default_rng(41)
@@ -358,7 +358,7 @@ def test_reduce_many_pipelined_matches_serial(S):
         S.set_overlap(0)
     for M, ref_band in zip(mats, bands):
         B = np.abs(M.cpu().numpy())
-        assert np.linalg.norm(B[inb] - ref_band[inb]) / np.linalg.norm(ref_band[inb]) < 1e-12
+        assert np.array_equal(B, ref_band)
         assert np.all(B[~inb] == 0)
 
 

@@ -17,6 +17,7 @@ int main(int argc, char **argv) {
     std::vector<double> h((size_t)n * n, 0.0);
     for (int i = 0; i < n; ++i) for (int j = i; j <= std::min(n - 1, i + b); ++j) h[(size_t)i * n + j] = 1.0 + ((i * 31 + j * 17) % 97) / 97.0;
     int *flags; (void)hipMalloc(&flags, sizeof(int) * (n + 2));
+    (void)hipMemset(flags, 0, sizeof(int) * (n + 2));
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     std::vector<unsigned long long> zero((size_t)4096 * 8, 0ull);
     for (int it = 0; it < 2; ++it) {

@@ -243,22 +243,22 @@ __device__ __forceinline__ void refl_apply(T (&a)[32], int L, WaveLds<T, EXACT> 
         }
         wave_sync2();
         const T tau = S.h[1];
-        T w[32];
-#pragma unroll
-        for (int c = 1; c < 32; ++c) w[c] = c < L ? S.w[c] : (T)0;
+        // w is read from LDS (broadcast) in both passes rather than held in
+        // registers: this edge-window path shares the kernel's register budget
+        // with the W-wave windows
         T d0 = a[0], d1 = (T)0, d2 = (T)0, d3 = (T)0;
 #pragma unroll
         for (int c = 1; c < 32; c += 4) {
-            d1 = fma(a[c], w[c], d1);
-            if (c + 1 < 32) d2 = fma(a[c + 1], w[c + 1], d2);
-            if (c + 2 < 32) d3 = fma(a[c + 2], w[c + 2], d3);
-            if (c + 3 < 32) d0 = fma(a[c + 3], w[c + 3], d0);
+            if (c < L) d1 = fma(a[c], S.w[c], d1);
+            if (c + 1 < 32 && c + 1 < L) d2 = fma(a[c + 1], S.w[c + 1], d2);
+            if (c + 2 < 32 && c + 2 < L) d3 = fma(a[c + 2], S.w[c + 2], d3);
+            if (c + 3 < 32 && c + 3 < L) d0 = fma(a[c + 3], S.w[c + 3], d0);
         }
         const T td = tau * ((d0 + d1) + (d2 + d3));
         a[0] -= td;
 #pragma unroll
         for (int c = 1; c < 32; ++c)
-            if (c < L) a[c] = fma(-td, w[c], a[c]);
+            if (c < L) a[c] = fma(-td, S.w[c], a[c]);
     } else {
 #pragma clang fp contract(off)
         if (lane == 0) {
@@ -419,23 +419,50 @@ __device__ __forceinline__ void win_left_full(const RingAcc<T> &A, int i1, int j
     }
 }
 
-// ---- full interior windows split over a PAIR of waves (fast mode, B = 32) -----
-// Each wave takes half of the window with TWO lanes per row (right window) or
-// per column (left window), each lane holding B/2 elements, so a window's
-// per-lane work -- and its latency on the stage-2 critical path -- halves.
-// The two lanes of a row / column are neighbours (lane ^ 1): partial dot
-// products and norms are combined by one DPP swap.  Both waves form the
-// reflector redundantly from the shared source row / column.
-template <typename T>
-__device__ __forceinline__ T swap1(T v);   // value of lane ^ 1 (DPP quad_perm [1,0,3,2])
+// ---- full interior windows split over W waves (fast mode, B = 32) -----------
+// A window's rows (right window) or columns (left window) get W lanes each,
+// every lane holding E = B / W consecutive elements of its row / column, so
+// the per-lane work of a window -- its latency on the stage-2 critical path --
+// drops by W.  The W lanes of a row / column are consecutive lanes of one
+// quad, so partial norms and dot products are combined by DPP (xor 1, xor 2)
+// without LDS.  Every lane forms the reflector's scalars itself (hardware
+// rsq / rcp refined by Newton steps).  Lane layout (L = 64 pw + lane, pw =
+// the wave's index within the sweep):
+//   right window rows [i1, i1+2B) x cols [j1, j1+B): row L / W, columns (L % W) E + [0, E)
+//   left window  rows [i1, i1+B) x cols [j1, j1+2B): column L / W, rows (L % W) E + [0, E)
+// Both are LDS-bank-conflict-free: element (r, c) of the ring sits at
+// dword 2 ((c - r) mod 32) modulo 64 (pitch 3b rounded to 16 B), and the 32
+// lanes of a half-wave touch 32 distinct c - r.
+// The source row / column (element group 0) belongs to wave pw = 0, which
+// must not store before the other waves have read it: they raise their
+// x-flag (tag) once their loads have returned, and wave 0 checks all flags
+// before its stores (MultiSync).
+template <typename T, int CTRL>
+__device__ __forceinline__ T dpp_mov(T v);
 template <>
-__device__ __forceinline__ double swap1<double>(double v) {
+__device__ __forceinline__ double dpp_mov<double, 0xB1>(double v) {
     return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0xB1, 0xf, 0xf, false),
                             __builtin_amdgcn_update_dpp(0, __double2loint(v), 0xB1, 0xf, 0xf, false));
 }
 template <>
-__device__ __forceinline__ float swap1<float>(float v) {
+__device__ __forceinline__ double dpp_mov<double, 0x4E>(double v) {
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x4E, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x4E, 0xf, 0xf, false));
+}
+template <>
+__device__ __forceinline__ float dpp_mov<float, 0xB1>(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));
+}
+template <>
+__device__ __forceinline__ float dpp_mov<float, 0x4E>(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));
+}
+// sum over the W consecutive lanes of a group (W = 1, 2, 4)
+template <int W, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+    if constexpr (W >= 2) v += dpp_mov<T, 0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (W >= 4) v += dpp_mov<T, 0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    return v;
 }
 // 1/sqrt(q) and 1/u: hardware estimate refined by Newton steps to full precision
 __device__ __forceinline__ double rsq_nr(double q) {
@@ -459,100 +486,106 @@ __device__ __forceinline__ float rcp_nr(float u) {
     const float y = __builtin_amdgcn_rcpf(u);
     return fmaf(y, fmaf(-u, y, 1.0f), y);
 }
-// Apply the reflector of x (x0 = the pivot, element 0 of the source vector) to
-// a; this lane holds elements [h*H, h*H + H) of both (h = lane & 1).
-template <typename T, int H>
-__device__ __forceinline__ void refl_apply_pair(T (&a)[H], const T (&x)[H], T x0, int h) {
-    T q[4] = {(T)0, (T)0, (T)0, (T)0}, sg[4] = {(T)0, (T)0, (T)0, (T)0};
+// Apply the reflector of the source vector x (x0 = its element 0, the pivot)
+// to a; this lane holds elements [q E, q E + E) of both.
+template <typename T, int E, int W>
+__device__ __forceinline__ void refl_apply_multi(T (&a)[E], const T (&x)[E], T x0, int q) {
+    T s2[4] = {(T)0, (T)0, (T)0, (T)0}, sg[4] = {(T)0, (T)0, (T)0, (T)0};
 #pragma unroll
-    for (int c = 0; c < H; ++c) q[c & 3] = fma(x[c], x[c], q[c & 3]);
+    for (int k = 0; k < E; ++k) s2[k & 3] = fma(x[k], x[k], s2[k & 3]);
 #pragma unroll
-    for (int c = 1; c < H; ++c) sg[c & 3] = fma(a[c], x[c], sg[c & 3]);
-    const T a0x0 = h ? a[0] * x[0] : (T)0;         // element 0 of the upper half is not the pivot
-    T qq = (q[0] + q[1]) + (q[2] + q[3]);
-    T sig = ((sg[0] + sg[1]) + (sg[2] + sg[3])) + a0x0;
-    qq += swap1(qq);
-    sig += swap1(sig);
-    const T a0o = swap1(a[0]);
-    const T a0 = h ? a0o : a[0];                     // the pivot-column element of this row / column
+    for (int k = 1; k < E; ++k) sg[k & 3] = fma(a[k], x[k], sg[k & 3]);
+    const bool piv = q == 0;                       // this lane holds element 0
+    if (!piv) sg[0] = fma(a[0], x[0], sg[0]);
+    const T qq = group_sum<W>((s2[0] + s2[1]) + (s2[2] + s2[3]));
+    const T sig = (sg[0] + sg[1]) + (sg[2] + sg[3]);
     const T rn = rsq_nr(qq);
     const T nrm = qq * rn;
     const T sgn = x0 >= (T)0 ? (T)-1 : (T)1;
     const T u1 = fma(-sgn, nrm, x0);
     const T alpha = rcp_nr(u1);
     const T tau = -sgn * u1 * rn;
-    const T td = tau * fma(alpha, sig, a0);
+    const T dot = group_sum<W>(fma(alpha, sig, piv ? a[0] : (T)0));   // w^T a, w_0 = 1, w_c = alpha x_c
+    const T td = tau * dot;
     const T tda = td * alpha;
-    const T e0 = h ? fma(-tda, x[0], a[0]) : a[0] - td;
+    const T e0 = piv ? a[0] - td : fma(-tda, x[0], a[0]);
 #pragma unroll
-    for (int c = 1; c < H; ++c) a[c] = fma(-tda, x[c], a[c]);
+    for (int k = 1; k < E; ++k) a[k] = fma(-tda, x[k], a[k]);
     a[0] = e0;
 }
 
-// right window rows [i1, i1+2B) x cols [j1, j1+B): this wave does rows
-// [i1 + half*B, i1 + half*B + B), lane -> row (lane >> 1), columns (lane & 1)*B/2 + [0, B/2)
-// The source row / column lies in half 0; the wave owning it (xo) must not
-// store before its partner has read the source: the partner raises its
-// x-flag (tag) once its loads have returned, the owner checks it before its
-// stores (PairSync).
-struct PairSync {
-    int *mine;            // this wave's x-flag
-    const int *partner;   // the partner's x-flag
-    int tag;
+struct MultiSync {
+    int *xr;      // x-flags of the sweep's W waves
+    int pw, W, tag;
     __device__ __forceinline__ void read_done(int lane) const {
+        if (pw == 0) return;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(mine, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(xr + pw, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __device__ __forceinline__ void before_store() const {
-        while (__hip_atomic_load(partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tag)
-            __builtin_amdgcn_s_sleep(0);
+        if (pw != 0) return;
+        for (int w = 1; w < W; ++w)
+            while (__hip_atomic_load(xr + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tag)
+                __builtin_amdgcn_s_sleep(0);
     }
 };
 
-template <typename T, int B>
-__device__ __forceinline__ void win_right_pair(const RingAcc<T> &A, int i1, int j1, int half, int lane,
-                                               const PairSync &ps) {
-    constexpr int H = B / 2;
-    const int h = lane & 1;
+// FULL = false: an edge window clipped to rows [i1, i2), cols [j1, j2) (right:
+// at most 2B x B, left: at most B x 2B); lanes and elements outside it hold
+// zeros, which leave the reflector and the dot products unchanged.
+template <typename T, int B, int W, bool FULL>
+__device__ __forceinline__ void win_right_multi(const RingAcc<T> &A, int i1, int i2, int j1, int j2, int L,
+                                                int lane, const MultiSync &ms) {
+    constexpr int E = B / W;
+    const int q = L % W, r = L / W;
+    const bool rok = FULL || i1 + r < i2;
     const T *px = A.row(i1) + j1;
-    T *pa = A.row(i1 + half * B + (lane >> 1)) + j1 + h * H;
-    T a[H], x[H];
+    T *pa = A.row(i1 + (rok ? r : 0)) + j1 + q * E;
+    T a[E], x[E];
 #pragma unroll
-    for (int c = 0; c < H; ++c) { x[c] = px[h * H + c]; a[c] = pa[c]; }
+    for (int k = 0; k < E; ++k) {
+        const bool cok = FULL || j1 + q * E + k < j2;
+        x[k] = cok ? px[q * E + k] : (T)0;
+        a[k] = (cok && rok) ? pa[k] : (T)0;
+    }
     const T x0 = px[0];
-    if (half != 0) ps.read_done(lane);
-    refl_apply_pair<T, H>(a, x, x0, h);
-    if (half == 0) ps.before_store();
+    ms.read_done(lane);
+    refl_apply_multi<T, E, W>(a, x, x0, q);
+    ms.before_store();
+    if (rok) {
 #pragma unroll
-    for (int c = 0; c < H; ++c) pa[c] = a[c];
+        for (int k = 0; k < E; ++k)
+            if (FULL || j1 + q * E + k < j2) pa[k] = a[k];
+    }
 }
 
-// left window rows [i1, i1+B) x cols [j1, j1+2B): this wave does columns
-// [j1 + half*B, j1 + half*B + B), lane -> column (lane >> 1), rows (lane & 1)*B/2 + [0, B/2)
-template <typename T, int B>
-__device__ __forceinline__ void win_left_pair(const RingAcc<T> &A, int i1, int j1, int half, int lane,
-                                              const PairSync &ps) {
-    constexpr int H = B / 2;
-    const int h = lane & 1;
-    const int col = half * B + (lane >> 1);
-    const int s0 = A.slot(i1), s1 = A.slot(i1 + H);
-    int slot = h ? s1 : s0;
-    const int r0 = i1 + h * H;
-    T a[H], x[H];
-    T *rows[H];
+template <typename T, int B, int W, bool FULL>
+__device__ __forceinline__ void win_left_multi(const RingAcc<T> &A, int i1, int i2, int j1, int j2, int L,
+                                               int lane, const MultiSync &ms) {
+    constexpr int E = B / W;
+    const int q = L % W, c = L / W;
+    const bool cok = FULL || j1 + c < j2;
+    const int col = cok ? c : 0;
+    int slot = A.slot(i1 + q * E);
+    T a[E], x[E];
+    T *rows[E];
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-        rows[k] = A.d + slot * A.P + A.off - (r0 + k) + j1;
-        x[k] = rows[k][0];
-        a[k] = rows[k][col];
+    for (int k = 0; k < E; ++k) {
+        const bool rk = FULL || i1 + q * E + k < i2;
+        rows[k] = A.d + slot * A.P + A.off - (i1 + q * E + k) + j1;
+        x[k] = rk ? rows[k][0] : (T)0;
+        a[k] = (rk && cok) ? rows[k][col] : (T)0;
         slot = slot + 1 == A.R ? 0 : slot + 1;
     }
     const T x0 = A.row(i1)[j1];
-    if (half != 0) ps.read_done(lane);
-    refl_apply_pair<T, H>(a, x, x0, h);
-    if (half == 0) ps.before_store();
+    ms.read_done(lane);
+    refl_apply_multi<T, E, W>(a, x, x0, q);
+    ms.before_store();
+    if (cok) {
 #pragma unroll
-    for (int k = 0; k < H; ++k) rows[k][col] = a[k];
+        for (int k = 0; k < E; ++k)
+            if (FULL || i1 + q * E + k < i2) rows[k][col] = a[k];
+    }
 }
 
 // ---- the reference's task list of one sweep --------------------------------
@@ -707,9 +740,19 @@ __device__ __forceinline__ void lds_rel(int *p, int v) {
 // bundle_plan); fp32 to S = 5 (512 threads).
 // W = compute waves per sweep: 2 on the b = 32 fast path (windows split over a
 // wave pair), else 1.
-template <bool EXACT, int KB> constexpr int bundle_w() { return (KB > 0 && !EXACT) ? 2 : 1; }
+// Threads of a bundle workgroup: W compute waves per sweep for up to 3 (fp64,
+// LDS-limited) or 5 (fp32) sweeps, plus the loader, writer and poller waves;
+// at most 1024.
 template <typename T, int W> constexpr int bundle_max_threads() {
-    return sizeof(T) == 8 ? (W == 2 ? 512 : 448) : (W == 2 ? 1024 : 512);
+    return 64 * (W * (sizeof(T) == 8 ? 3 : 5) + 3) < 1024 ? 64 * (W * (sizeof(T) == 8 ? 3 : 5) + 3) : 1024;
+}
+// smallest progress count of the W waves of one sweep
+template <int W>
+__device__ __forceinline__ int prog_min(const int *p) {
+    int m = lds_acq(p);
+#pragma unroll
+    for (int w = 1; w < W; ++w) m = min(m, lds_acq(p + w));
+    return m;
 }
 constexpr int kWriteRows = 32;  // rows per writer batch (at most)
 constexpr int kSubRows = 8;     // rows per writer sub-chunk (registers)
@@ -780,13 +823,17 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
 
 template <typename T, bool EXACT, int KB, int W>
 __global__ void __launch_bounds__((bundle_max_threads<T, W>()))
-k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
+k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, int Q, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int P = ring_pitch<T>(b);
     T *ring = (T *)smem;
     const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
-    WaveLds<T, EXACT> *wl = (WaveLds<T, EXACT> *)(smem + ring_bytes);
+    // Q > 0: the loader's staging queue of Q rows right after the ring (rows are
+    // fetched into it as soon as the previous bundle has written them, and
+    // copied into their ring slot once the writer has freed it)
+    T *stage = (T *)(smem + ring_bytes);
+    WaveLds<T, EXACT> *wl = (WaveLds<T, EXACT> *)(smem + ring_bytes + (size_t)Q * P * sizeof(T));
     BundleFlags *F = (BundleFlags *)(wl + S);
     // readfirstlane: the compiler then keeps all window geometry in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -811,11 +858,12 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
 
         if (wave < W * nsw) {
             // ---------------- compute wave(s): sweep i0 + sw ----------------
-            // W = 2: waves 2sw (pw = 0) and 2sw + 1 (pw = 1) share the sweep; full
-            // windows are split between them (win_*_pair), the others run on
-            // wave pw = 0 alone.  Before task t a wave waits for its partner to
-            // finish task t - 1 (a window's reflector source comes from the
-            // partner's half of the previous window).
+            // W waves per sweep (waves W sw .. W sw + W - 1, pw = 0 .. W-1): full
+            // windows are split over them (win_*_multi), the others run on wave
+            // pw = 0 alone.  Before task t every wave waits for all W waves of its
+            // sweep to finish task t - 1 (a window reads what the whole previous
+            // window wrote) and, by the lag-3 rule, for all W waves of the
+            // previous sweep to finish task t + 3.
             const int sw = wave / W, pw = wave - sw * W;
             const int i = i0 + sw;
             SweepIter it;
@@ -830,20 +878,13 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                 S2TT(beta, wave, t, 0);
                 if (sw > 0) {
                     const int need = min(t + 4, prev_ntask);
-                    if constexpr (W == 2) {
-                        while (min(lds_acq(&F->prog[2 * sw - 2]), lds_acq(&F->prog[2 * sw - 1])) < need) {
-                            __builtin_amdgcn_s_sleep(1);
-                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
-                        }
-                    } else {
-                        while (lds_acq(&F->prog[sw - 1]) < need) {
-                            __builtin_amdgcn_s_sleep(1);
-                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
-                        }
+                    while (prog_min<W>(F->prog + W * (sw - 1)) < need) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
                     }
                 }
-                if constexpr (W == 2) {
-                    while (lds_acq(&F->prog[wave ^ 1]) < t) {
+                if constexpr (W > 1) {
+                    while (prog_min<W>(F->prog + W * sw) < t) {
                         __builtin_amdgcn_s_sleep(0);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 7); break; }
                     }
@@ -863,14 +904,15 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     if constexpr (KB > 0) {
                         const bool full_r = right && wr == 2 * KB && wc == KB;
                         const bool full_l = !right && wr == KB && wc == 2 * KB;
-                        if constexpr (W == 2) {
-                            const PairSync ps{&F->xr[wave], &F->xr[wave ^ 1], t + 1};
-                            if (full_r) win_right_pair<T, KB>(acc, wnd.i1, wnd.j1, pw, lane, ps);
-                            else if (full_l) win_left_pair<T, KB>(acc, wnd.i1, wnd.j1, 1 - pw, lane, ps);
-                            else if (pw == 0) {
-                                if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                                else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                            }
+                        if constexpr (W > 1) {
+                            // every window of the sweep on all W waves: full ones
+                            // unpredicated, clipped edge windows predicated
+                            const MultiSync ms{F->xr + W * sw, pw, W, t + 1};
+                            const int L = 64 * pw + lane;
+                            if (full_r) win_right_multi<T, KB, W, true>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
+                            else if (full_l) win_left_multi<T, KB, W, true>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
+                            else if (right) win_right_multi<T, KB, W, false>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
+                            else            win_left_multi<T, KB, W, false>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
                         } else {
                             if (full_r) win_right_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
                             else if (full_l) win_left_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
@@ -896,6 +938,95 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
             }
             if (lane == 0 && wave == 0) S2STAMP(beta, 2);
             if (lane == 0 && wave == W * nsw - 1) S2STAMP(beta, 3);
+        } else if (wave == W * S && Q > 0) {
+            // ---------------- loader wave, staged: HBM -> staging queue -> ring ----------------
+            // Rows are fetched by LDS-DMA (one global_load_lds_dwordx4 per
+            // interior row, sc1) into staging slot r % Q as soon as bundle beta-1
+            // has written them back (`avail`) and the slot's previous row has been
+            // copied out, independent of the ring.  A row is copied staging ->
+            // ring (one ds_read_b128 + ds_write_b128 per lane) once it has landed
+            // (counted vmcnt: DMAs complete in issue order) and its ring slot is
+            // free (`freed`), then published (`loaded`).  So a slot freed by the
+            // writer is refilled at LDS speed instead of after a memory round trip
+            // (Stage 2).  Edge rows (columns outside the matrix) are
+            // loaded synchronously through registers into their staging slot.
+            const int row_q = P * (int)sizeof(T) / 16;
+            const unsigned row_bytes = (unsigned)(P * (int)sizeof(T));
+            const unsigned stage_lds = (unsigned)(uintptr_t)stage;
+            const int dma_hi = (int)(((long)(n - 1) * lda + n + (b - 1) - P) / (lda + 1));
+            const bool dma_lane = lane < row_q;
+            const long rstep = (lda + 1) * (long)sizeof(T);
+            int rs = i0, rc = i0, ndma = 0, spins = 0;   // ndma: DMAs issued, not yet known landed (rows rs-ndma..rs-1)
+            int qs = 0;                                   // staging slot of row rs (= rs % Q, kept incrementally)
+            const char *src = (const char *)(A + (long)i0 * lda + i0 - (b - 1)) + 16 * lane;
+            int qc = 0, rslot = acc.slot(i0);             // staging slot / ring slot of row rc
+            while (rc < n) {
+                const int av = __hip_atomic_load(&F->avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int fr = __hip_atomic_load(&F->freed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                bool moved = false;
+                // (1) fetch into staging
+                const int lim = __builtin_amdgcn_readfirstlane(min(min(av, rc + Q), n));
+                if (rs < lim) {
+                    if (rs >= 1 && rs <= dma_hi) {
+                        const int k = min(lim, dma_hi + 1) - rs;
+                        if (dma_lane) {
+                            const char *p = src;
+                            int q = qs;
+                            for (int i = 0; i < k; ++i) {
+                                dma16_sc1(p, stage_lds + (unsigned)q * row_bytes);
+                                p += rstep;
+                                q = q + 1 == Q ? 0 : q + 1;
+                            }
+                        }
+                        src += (long)k * rstep;
+                        qs = (qs + k) % Q;
+                        rs += k;
+                        ndma += k;
+                        moved = true;
+                    } else {   // edge row: after every DMA before it has landed
+                        load_edge_row<T>(A, lda, n, b, rs, stage + (size_t)qs * P, row_q, lane);
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        ndma = 0;
+                        ++rs;
+                        src += rstep;
+                        qs = qs + 1 == Q ? 0 : qs + 1;
+                        moved = true;
+                    }
+                }
+                // (2) landed rows into free ring slots
+                const int k = __builtin_amdgcn_readfirstlane(min(rs, fr + R) - rc);
+                if (k > 0) {
+                    const int keep = rs - (rc + k);   // younger rows whose DMAs may stay in flight
+                    if (keep < ndma) {
+                        wait_vmcnt(keep);
+                        ndma = keep;
+                    }
+                    if (lane < row_q) {
+                        int q = qc, sl = rslot;
+                        for (int i = 0; i < k; ++i) {
+                            const u32x4 v = *((const u32x4 *)(stage + (size_t)q * P) + lane);
+                            *((u32x4 *)(ring + (size_t)sl * P) + lane) = v;
+                            q = q + 1 == Q ? 0 : q + 1;
+                            sl = sl + 1 == R ? 0 : sl + 1;
+                        }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    rc += k;
+                    qc = (qc + k) % Q;
+                    rslot = (rslot + k) % R;
+                    if (lane == 0) lds_rel(&F->loaded, rc);
+                    S2PUB(beta, 0, rc);
+                    moved = true;
+                }
+                if (moved) {
+                    spins = 0;
+                } else {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 4); break; }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) S2STAMP(beta, 5);
         } else if (wave == W * S) {
             // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
             // An interior row (all P columns inside the matrix) is copied by ONE
@@ -1116,13 +1247,39 @@ __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
 int ring_min_rows(int b, int S) { return ((3 * (S - 1)) / 2 + 2) * b + S + 8; }
 
 template <typename T, bool EXACT>
-static size_t bundle_lds_bytes(int b, int S, int R) {
+static size_t bundle_lds_bytes(int b, int S, int R, int Q) {
     const size_t ring = ((size_t)R * ring_pitch<T>(b) * sizeof(T) + 15) & ~(size_t)15;
-    return ring + (size_t)S * sizeof(WaveLds<T, EXACT>) + sizeof(BundleFlags);
+    return ring + (size_t)Q * ring_pitch<T>(b) * sizeof(T) + (size_t)S * sizeof(WaveLds<T, EXACT>) +
+           sizeof(BundleFlags);
+}
+
+// Compute waves per sweep on the b = 32 fast path (BRD_S2_W: 1, 2 or 4).
+// Measured at N = 8192 fp64 (3 sweeps per bundle, same box): W = 1 96.5 ms,
+// W = 2 90.9 ms, W = 4 114.5 ms -- four waves per window pay more in
+// per-task synchronisation (all W waves of a sweep meet before every task)
+// than they save in window latency.
+static int s2_waves_per_sweep() {
+    static int w = 0;
+    if (!w) {
+        const char *e = getenv("BRD_S2_W");
+        const int v = e ? atoi(e) : 2;
+        w = (v == 1 || v == 2 || v == 4) ? v : 2;
+    }
+    return w;
+}
+
+// Loader staging rows (BRD_S2_STAGE; 0 = rows DMA'd straight into ring slots).
+static int stage_rows() {
+    static int q = -1;
+    if (q < 0) {
+        const char *e = getenv("BRD_S2_STAGE");
+        q = e ? std::max(0, std::min(48, atoi(e))) : 0;
+    }
+    return q;
 }
 
 template <typename T, bool EXACT, int W>
-static bool bundle_plan(int n, int b, int &S, int &R) {
+static bool bundle_plan(int n, int b, int Q, int &S, int &R) {
     const size_t budget = 160 * 1024 - 512;
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
     int smax = EXACT ? 2 : (bundle_max_threads<T, W>() / 64 - 3) / W;
@@ -1135,12 +1292,12 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
     for (int slack : {forced ? 8 : 16, 8}) {
         for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
             const int rmin = ring_min_rows(b, S) + slack;
-            if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
+            if (bundle_lds_bytes<T, EXACT>(b, S, rmin, Q) <= budget) {
                 // largest ring that fits, but no more than n rows
                 static const char *renv = getenv("BRD_S2_RING");   // tuning: cap on ring rows
                 const int rcap = renv && atoi(renv) > 0 ? std::max(rmin, atoi(renv)) : 1 << 30;
                 R = rmin;
-                while (R < n + 1 && R + 8 <= rcap && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
+                while (R < n + 1 && R + 8 <= rcap && bundle_lds_bytes<T, EXACT>(b, S, R + 8, Q) <= budget) R += 8;
                 return true;
             }
         }
@@ -1173,33 +1330,37 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
     const bool pipe = sel && sel[0] == 'p';
     int S = 0, R = 0;
     const bool fast32 = !exact_order && b == 32;
-    static const char *penv = getenv("BRD_S2_PAIR");    // tuning: "1" = wave pairs per sweep on the b = 32 path
-    const int W = fast32 && penv && penv[0] == '1' ? 2 : 1;
-    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, S, R)
-                    : W == 2    ? bundle_plan<T, false, 2>(n, b, S, R)
-                                : bundle_plan<T, false, 1>(n, b, S, R);
+    const int W = fast32 ? s2_waves_per_sweep() : 1;
+    const int Q = stage_rows();
+    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, Q, S, R)
+                    : W == 4    ? bundle_plan<T, false, 4>(n, b, Q, S, R)
+                    : W == 2    ? bundle_plan<T, false, 2>(n, b, Q, S, R)
+                                : bundle_plan<T, false, 1>(n, b, Q, S, R);
     if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule
         const int nbundles = (n - 1 + S - 1) / S;
         const dim3 block(64 * (W * S + 3));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
         const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0, 1>
+                         : W == 4    ? (const void *)k_band2bd_bundle<T, false, 32, 4>
                          : W == 2    ? (const void *)k_band2bd_bundle<T, false, 32, 2>
                          : fast32    ? (const void *)k_band2bd_bundle<T, false, 32, 1>
                                      : (const void *)k_band2bd_bundle<T, false, 0, 1>;
-        const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
+        const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R, Q) : bundle_lds_bytes<T, false>(b, S, R, Q);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         const int cap = coresident_limit(fn, (int)block.x, lds);
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+        else if (W == 4)
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
         else if (W == 2)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
         else if (fast32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
         return hipGetLastError();
     }
     const void *pfn = exact_order ? (const void *)k_band2bd_pipe<T, true> : (const void *)k_band2bd_pipe<T, false>;

@@ -243,22 +243,22 @@ __device__ __forceinline__ void refl_apply(T (&a)[32], int L, WaveLds<T, EXACT> 
         }
         wave_sync2();
         const T tau = S.h[1];
-        // w is read from LDS (broadcast) in both passes rather than held in
-        // registers: this edge-window path shares the kernel's register budget
-        // with the W-wave windows
+        T w[32];
+#pragma unroll
+        for (int c = 1; c < 32; ++c) w[c] = c < L ? S.w[c] : (T)0;
         T d0 = a[0], d1 = (T)0, d2 = (T)0, d3 = (T)0;
 #pragma unroll
         for (int c = 1; c < 32; c += 4) {
-            if (c < L) d1 = fma(a[c], S.w[c], d1);
-            if (c + 1 < 32 && c + 1 < L) d2 = fma(a[c + 1], S.w[c + 1], d2);
-            if (c + 2 < 32 && c + 2 < L) d3 = fma(a[c + 2], S.w[c + 2], d3);
-            if (c + 3 < 32 && c + 3 < L) d0 = fma(a[c + 3], S.w[c + 3], d0);
+            d1 = fma(a[c], w[c], d1);
+            if (c + 1 < 32) d2 = fma(a[c + 1], w[c + 1], d2);
+            if (c + 2 < 32) d3 = fma(a[c + 2], w[c + 2], d3);
+            if (c + 3 < 32) d0 = fma(a[c + 3], w[c + 3], d0);
         }
         const T td = tau * ((d0 + d1) + (d2 + d3));
         a[0] -= td;
 #pragma unroll
         for (int c = 1; c < 32; ++c)
-            if (c < L) a[c] = fma(-td, S.w[c], a[c]);
+            if (c < L) a[c] = fma(-td, w[c], a[c]);
     } else {
 #pragma clang fp contract(off)
         if (lane == 0) {
@@ -823,17 +823,13 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
 
 template <typename T, bool EXACT, int KB, int W>
 __global__ void __launch_bounds__((bundle_max_threads<T, W>()))
-k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, int Q, unsigned magic, int *rows_done, int *err)
+k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int P = ring_pitch<T>(b);
     T *ring = (T *)smem;
     const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
-    // Q > 0: the loader's staging queue of Q rows right after the ring (rows are
-    // fetched into it as soon as the previous bundle has written them, and
-    // copied into their ring slot once the writer has freed it)
-    T *stage = (T *)(smem + ring_bytes);
-    WaveLds<T, EXACT> *wl = (WaveLds<T, EXACT> *)(smem + ring_bytes + (size_t)Q * P * sizeof(T));
+    WaveLds<T, EXACT> *wl = (WaveLds<T, EXACT> *)(smem + ring_bytes);
     BundleFlags *F = (BundleFlags *)(wl + S);
     // readfirstlane: the compiler then keeps all window geometry in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -938,95 +934,6 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, int Q, u
             }
             if (lane == 0 && wave == 0) S2STAMP(beta, 2);
             if (lane == 0 && wave == W * nsw - 1) S2STAMP(beta, 3);
-        } else if (wave == W * S && Q > 0) {
-            // ---------------- loader wave, staged: HBM -> staging queue -> ring ----------------
-            // Rows are fetched by LDS-DMA (one global_load_lds_dwordx4 per
-            // interior row, sc1) into staging slot r % Q as soon as bundle beta-1
-            // has written them back (`avail`) and the slot's previous row has been
-            // copied out, independent of the ring.  A row is copied staging ->
-            // ring (one ds_read_b128 + ds_write_b128 per lane) once it has landed
-            // (counted vmcnt: DMAs complete in issue order) and its ring slot is
-            // free (`freed`), then published (`loaded`).  So a slot freed by the
-            // writer is refilled at LDS speed instead of after a memory round trip
-            // (Stage 2).  Edge rows (columns outside the matrix) are
-            // loaded synchronously through registers into their staging slot.
-            const int row_q = P * (int)sizeof(T) / 16;
-            const unsigned row_bytes = (unsigned)(P * (int)sizeof(T));
-            const unsigned stage_lds = (unsigned)(uintptr_t)stage;
-            const int dma_hi = (int)(((long)(n - 1) * lda + n + (b - 1) - P) / (lda + 1));
-            const bool dma_lane = lane < row_q;
-            const long rstep = (lda + 1) * (long)sizeof(T);
-            int rs = i0, rc = i0, ndma = 0, spins = 0;   // ndma: DMAs issued, not yet known landed (rows rs-ndma..rs-1)
-            int qs = 0;                                   // staging slot of row rs (= rs % Q, kept incrementally)
-            const char *src = (const char *)(A + (long)i0 * lda + i0 - (b - 1)) + 16 * lane;
-            int qc = 0, rslot = acc.slot(i0);             // staging slot / ring slot of row rc
-            while (rc < n) {
-                const int av = __hip_atomic_load(&F->avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int fr = __hip_atomic_load(&F->freed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                bool moved = false;
-                // (1) fetch into staging
-                const int lim = __builtin_amdgcn_readfirstlane(min(min(av, rc + Q), n));
-                if (rs < lim) {
-                    if (rs >= 1 && rs <= dma_hi) {
-                        const int k = min(lim, dma_hi + 1) - rs;
-                        if (dma_lane) {
-                            const char *p = src;
-                            int q = qs;
-                            for (int i = 0; i < k; ++i) {
-                                dma16_sc1(p, stage_lds + (unsigned)q * row_bytes);
-                                p += rstep;
-                                q = q + 1 == Q ? 0 : q + 1;
-                            }
-                        }
-                        src += (long)k * rstep;
-                        qs = (qs + k) % Q;
-                        rs += k;
-                        ndma += k;
-                        moved = true;
-                    } else {   // edge row: after every DMA before it has landed
-                        load_edge_row<T>(A, lda, n, b, rs, stage + (size_t)qs * P, row_q, lane);
-                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                        ndma = 0;
-                        ++rs;
-                        src += rstep;
-                        qs = qs + 1 == Q ? 0 : qs + 1;
-                        moved = true;
-                    }
-                }
-                // (2) landed rows into free ring slots
-                const int k = __builtin_amdgcn_readfirstlane(min(rs, fr + R) - rc);
-                if (k > 0) {
-                    const int keep = rs - (rc + k);   // younger rows whose DMAs may stay in flight
-                    if (keep < ndma) {
-                        wait_vmcnt(keep);
-                        ndma = keep;
-                    }
-                    if (lane < row_q) {
-                        int q = qc, sl = rslot;
-                        for (int i = 0; i < k; ++i) {
-                            const u32x4 v = *((const u32x4 *)(stage + (size_t)q * P) + lane);
-                            *((u32x4 *)(ring + (size_t)sl * P) + lane) = v;
-                            q = q + 1 == Q ? 0 : q + 1;
-                            sl = sl + 1 == R ? 0 : sl + 1;
-                        }
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    rc += k;
-                    qc = (qc + k) % Q;
-                    rslot = (rslot + k) % R;
-                    if (lane == 0) lds_rel(&F->loaded, rc);
-                    S2PUB(beta, 0, rc);
-                    moved = true;
-                }
-                if (moved) {
-                    spins = 0;
-                } else {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 4); break; }
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) S2STAMP(beta, 5);
         } else if (wave == W * S) {
             // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
             // An interior row (all P columns inside the matrix) is copied by ONE
@@ -1247,10 +1154,9 @@ __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
 int ring_min_rows(int b, int S) { return ((3 * (S - 1)) / 2 + 2) * b + S + 8; }
 
 template <typename T, bool EXACT>
-static size_t bundle_lds_bytes(int b, int S, int R, int Q) {
+static size_t bundle_lds_bytes(int b, int S, int R) {
     const size_t ring = ((size_t)R * ring_pitch<T>(b) * sizeof(T) + 15) & ~(size_t)15;
-    return ring + (size_t)Q * ring_pitch<T>(b) * sizeof(T) + (size_t)S * sizeof(WaveLds<T, EXACT>) +
-           sizeof(BundleFlags);
+    return ring + (size_t)S * sizeof(WaveLds<T, EXACT>) + sizeof(BundleFlags);
 }
 
 // Compute waves per sweep on the b = 32 fast path (BRD_S2_W: 1, 2 or 4).
@@ -1268,18 +1174,8 @@ static int s2_waves_per_sweep() {
     return w;
 }
 
-// Loader staging rows (BRD_S2_STAGE; 0 = rows DMA'd straight into ring slots).
-static int stage_rows() {
-    static int q = -1;
-    if (q < 0) {
-        const char *e = getenv("BRD_S2_STAGE");
-        q = e ? std::max(0, std::min(48, atoi(e))) : 0;
-    }
-    return q;
-}
-
 template <typename T, bool EXACT, int W>
-static bool bundle_plan(int n, int b, int Q, int &S, int &R) {
+static bool bundle_plan(int n, int b, int &S, int &R) {
     const size_t budget = 160 * 1024 - 512;
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
     int smax = EXACT ? 2 : (bundle_max_threads<T, W>() / 64 - 3) / W;
@@ -1292,12 +1188,12 @@ static bool bundle_plan(int n, int b, int Q, int &S, int &R) {
     for (int slack : {forced ? 8 : 16, 8}) {
         for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
             const int rmin = ring_min_rows(b, S) + slack;
-            if (bundle_lds_bytes<T, EXACT>(b, S, rmin, Q) <= budget) {
+            if (bundle_lds_bytes<T, EXACT>(b, S, rmin) <= budget) {
                 // largest ring that fits, but no more than n rows
                 static const char *renv = getenv("BRD_S2_RING");   // tuning: cap on ring rows
                 const int rcap = renv && atoi(renv) > 0 ? std::max(rmin, atoi(renv)) : 1 << 30;
                 R = rmin;
-                while (R < n + 1 && R + 8 <= rcap && bundle_lds_bytes<T, EXACT>(b, S, R + 8, Q) <= budget) R += 8;
+                while (R < n + 1 && R + 8 <= rcap && bundle_lds_bytes<T, EXACT>(b, S, R + 8) <= budget) R += 8;
                 return true;
             }
         }
@@ -1331,11 +1227,10 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
     int S = 0, R = 0;
     const bool fast32 = !exact_order && b == 32;
     const int W = fast32 ? s2_waves_per_sweep() : 1;
-    const int Q = stage_rows();
-    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, Q, S, R)
-                    : W == 4    ? bundle_plan<T, false, 4>(n, b, Q, S, R)
-                    : W == 2    ? bundle_plan<T, false, 2>(n, b, Q, S, R)
-                                : bundle_plan<T, false, 1>(n, b, Q, S, R);
+    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, S, R)
+                    : W == 4    ? bundle_plan<T, false, 4>(n, b, S, R)
+                    : W == 2    ? bundle_plan<T, false, 2>(n, b, S, R)
+                                : bundle_plan<T, false, 1>(n, b, S, R);
     if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule
         const int nbundles = (n - 1 + S - 1) / S;
         const dim3 block(64 * (W * S + 3));
@@ -1345,22 +1240,22 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
                          : W == 2    ? (const void *)k_band2bd_bundle<T, false, 32, 2>
                          : fast32    ? (const void *)k_band2bd_bundle<T, false, 32, 1>
                                      : (const void *)k_band2bd_bundle<T, false, 0, 1>;
-        const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R, Q) : bundle_lds_bytes<T, false>(b, S, R, Q);
+        const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         const int cap = coresident_limit(fn, (int)block.x, lds);
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 4)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 2)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (fast32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, Q, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const void *pfn = exact_order ? (const void *)k_band2bd_pipe<T, true> : (const void *)k_band2bd_pipe<T, false>;

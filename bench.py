@@ -81,8 +81,9 @@ def parse():
                    help="pipelined: CUs reserved for stage 2 (default svdsolver_amd.overlap_cus(n))")
     p.add_argument("--one-at-a-time", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: also time K steps without the overlap (reported as one_at_a_time)")
-    p.add_argument("--lanes", type=int, default=1,
-                   help="pipelined, one GPU: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L")
+    p.add_argument("--lanes", type=int, default=None,
+                   help="pipelined, one GPU: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
+                        "(default 4; 1 across GPUs)")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -281,6 +282,14 @@ def maybe_spawn(args) -> None:
 
 def main():
     args = parse()
+    if args.lanes is None:
+        args.lanes = 4 if ("WORLD_SIZE" not in os.environ and args.gpus <= 1) else 1
+    # Every lane launches on two HIP streams; with the runtime's default of 4
+    # hardware queues per process, streams beyond that share a queue and
+    # their work serialises (measured: 2 lanes 14.1 -> 17.8 TFLOP/s once each
+    # stream has a queue).  Read when the HIP runtime initialises, so set first.
+    if args.lanes > 1:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, 2 * args.lanes + 4)))
     maybe_spawn(args)
     import torch
     import torch.distributed as dist
@@ -375,11 +384,11 @@ def main():
     # few dozen CUs, stage 1 HBM-bound on the rest); otherwise s_b's work is
     # ordered after all of s_a's and vice versa (one reduction at a time).
     # --lanes L > 1 (one GPU): L such pipelines side by side, matrix j on lane
-    # j mod L (the library keeps a workspace per launch stream), meant to let
-    # one lane's latency-bound panel factors overlap another lane's HBM-bound
-    # trailing updates.  Measured at N = 8192 (8 steps): L = 2 14.1 TFLOP/s vs
-    # 13.9 for L = 1, L = 3 11.6 -- the lanes' launches mostly take turns on
-    # the CUs instead of sharing them, so the default stays 1.
+    # j mod L (the library keeps a workspace per launch stream), so one lane's
+    # latency-bound tail panels and stage-2 chase overlap another lane's
+    # HBM-bound trailing updates.  Measured at N = 8192 fp64 (20 steps, one
+    # hardware queue per stream): L = 1 14.1 TFLOP/s, L = 2 18.2, L = 4 19.9,
+    # L = 8 20.3 -- default 4 (memory: warmup + 2K matrices resident).
     lanes = args.lanes if (pipelined and not dist_mode) else 1
     sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
     sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
@@ -439,24 +448,28 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.comm == "rccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # (2) the same steps again with the library's per-launch HIP events on
-    # its launch streams: kernel durations for the roofline object
-    S.profile_reset()
-    S.profile_enable(True)
-    el_prof, _, _ = run_steps(args.warmup + args.steps)
-    S.profile_enable(False)
     one_at_a_time = None
     if serial_too:
-        # (3) the same kind of steps without the overlap (whole chip per stage):
-        # the latency of one reduction, reported beside the stream's throughput
+        # (2) the same kind of steps without any overlap (one reduction at a
+        # time, whole chip per stage): the latency of one reduction, reported
+        # beside the stream's throughput
         mode["pipe"] = False
         S.set_overlap(0)
-        el_s, s1_s, s2_s = run_steps(args.warmup + 2 * args.steps)
-        S.set_overlap(s2_cus)
-        mode["pipe"] = True
+        el_s, s1_s, s2_s = run_steps(args.warmup + args.steps)
         one_at_a_time = {"value": round(args.steps * 8.0 / 3.0 * n ** 3 / el_s / 1e9, 2),
                          "ms_per_step": round(el_s / args.steps * 1e3, 3),
                          "stage_ms": {"stage1": round(s1_s, 3), "stage2": round(s2_s, 3)}}
+    # (3) K steps with the library's per-launch HIP events on its launch
+    # streams: kernel durations for the roofline object.  On one GPU they run
+    # one reduction at a time (as in (2)), so a kernel's duration is its own,
+    # not stretched by the concurrent lanes of (1); across GPUs they repeat (1).
+    S.profile_reset()
+    S.profile_enable(True)
+    el_prof, _, _ = run_steps(args.warmup + (2 if serial_too else 1) * args.steps)
+    S.profile_enable(False)
+    if serial_too:
+        S.set_overlap(s2_cus)
+        mode["pipe"] = True
     ap = S.profile_query("s1_apply")
     fa = S.profile_query("s1_factor")
     sw = S.profile_query("s2_sweep")
@@ -483,9 +496,11 @@ def main():
                                    + f", band {b}, "
                                    + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
                                       else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
-                       "value_kind": ("stream throughput: K matrices back to back, stage 2 of matrix i beside stage 1 "
-                                      "of matrix i+1 (per-reduction latency: latency_ms_per_reduction; one reduction "
-                                      "at a time: one_at_a_time)" if pipelined else "one reduction at a time"),
+                       "value_kind": (f"stream throughput: K independent matrices issued back to back on {lanes} "
+                                      "lane(s) of HIP streams (matrix j on lane j mod lanes; per lane stage 2 of "
+                                      "matrix i beside stage 1 of the next), fill and drain inside the timed region; "
+                                      "per-reduction latency under overlap: latency_ms_per_reduction; one reduction "
+                                      "at a time: one_at_a_time" if pipelined else "one reduction at a time"),
                        "n": n, "band": b, "global_batch": matrices,
                        "matrices_per_timed_region": matrices * args.steps,
                        "parallelism": (f"stage1 block-cyclic columns over {world} GPUs ({'RCCL' if args.comm == 'rccl' else 'host gloo'}), stage2 on rank "
@@ -499,6 +514,7 @@ def main():
             "one_at_a_time": one_at_a_time,
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
+            "profiled_pass": "one reduction at a time" if serial_too else "as the timed steps",
             "roofline": apply_roofline(ap, args.dtype, n),
             "stage2": stage2_roofline(sw, n, b, args.dtype, args.steps),
             "kernel_ms_per_step": {"s1_apply": round(ap["ms"] / args.steps, 3),

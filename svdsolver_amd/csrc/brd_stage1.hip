@@ -511,6 +511,24 @@ constexpr int kAW = kAT / 64;               // waves
 constexpr int kAB = (kRmax / 16) / kAW;     // 16-row blocks per wave
 constexpr int kXN = kRmax * kASlab / kAT;   // slab elements staged per thread
 
+// Raw buffer access (32-bit byte offsets; out-of-range offsets read 0 and
+// drop stores).
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+template <> __device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+template <typename T> __device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
+}
+template <> __device__ __forceinline__ void buf_store<float>(float v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+
 template <bool TR>
 __device__ __forceinline__ int xidx(int r, int c) {
     return TR ? c * kPT + r : r * kASlab + c;
@@ -622,7 +640,7 @@ struct ApplyLds {
 };
 
 // The apply of node grp to slab run `run` (k_apply, or the apply role of k_apply_factor).
-template <typename T, bool TR>
+template <typename T, bool TR, bool DIRECT>
 __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const int run, T *__restrict__ base, long ld,
                                            LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
                                            const T *__restrict__ VTws, const T *__restrict__ Tws)
@@ -668,6 +686,116 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
     }
     __syncthreads();
 
+    // ---- the W reduction and W2 = -(T^T W), shared by both slab paths -------
+    // acc: this wave's partial W (two 16 x 16 tiles); afterwards sW2 holds W2
+    // and the caller reads it after its lds_barrier.
+    auto reduce_w2 = [&](v4 (&acc)[2]) {
+        if (w < nblk) {
+#pragma unroll
+            for (int ab = 0; ab < 2; ++ab)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) sWp[w][(ab * 16 + q + 4 * g) * 16 + l15] = acc[ab][g];
+        }
+        lds_barrier();
+        // cross-wave sum in wave order: the result does not depend on which
+        // wave finishes first (stage 1 is bitwise reproducible run to run)
+        {
+            const int nwp = min(kAW, nblk);
+            T sum = sWp[0][tid];
+            for (int k = 1; k < nwp; ++k) sum += sWp[k][tid];
+            sW[(tid >> 4) * 17 + (tid & 15)] = sum;
+        }
+        lds_barrier();
+        if (w < 2) {
+            const int ab = w;
+            v4 a2 = {0, 0, 0, 0};
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const int k = 4 * st + q;
+                a2 = Mfma<T>::mma(sT[k * 32 + ab * 16 + arw], sW[k * 17 + l15], a2);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) sW2[(ab * 16 + q + 4 * g) * 17 + l15] = -a2[g];
+        }
+        lds_barrier();
+    };
+
+    if constexpr (DIRECT) {
+        static_assert(!TR, "the register-resident slab path is for the row-major view");
+        {
+            // ---- row-major view: the slab never touches LDS ----------------
+            // The B operand of W = V^T X at step s of row block jb is
+            // X[blk*16 + q + 4s][l15], and the accumulator register g of the
+            // update X += V W2 is X[blk*16 + q + 4g][l15]: the same element, so
+            // one register tile x[jb][.] is loaded from HBM (16 lanes = one
+            // 128-byte row segment), feeds both MFMA phases and is stored back.
+            // The next slab's tile is in flight while this one computes.
+            // the 16 rows of a block are consecutive matrix rows (launch_apply
+            // takes this path only when every tree node is made of whole
+            // 16-row blocks): one byte offset per block, rows blk*16 + q + 4g.
+            // Buffer loads / stores with 32-bit offsets (the view is < 4 GiB):
+            // an offset past the end (rows beyond the node, columns beyond the
+            // slab) reads 0 and drops the store, so no lane predicates.
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+            constexpr unsigned kOut = 0x80000000u;   // >= num_records: out of range
+            unsigned rb[kAB];
+#pragma unroll
+            for (int jb = 0; jb < kAB; ++jb) {
+                const int b16 = (w + kAW * jb) * 16;
+                rb[jb] = b16 < nr ? (unsigned)((sMap[b16] + q) * (int)ld + l15) * (unsigned)sizeof(T) : kOut;
+            }
+            const unsigned ld4b = 4u * (unsigned)ld * (unsigned)sizeof(T);
+            auto off = [&](int jb, int g, int c0, int nc) -> unsigned {
+                const bool ok = l15 < nc && (w + kAW * jb) * 16 + q + 4 * g < nr;
+                return ok ? rb[jb] + (unsigned)g * ld4b + (unsigned)c0 * (unsigned)sizeof(T) : kOut;
+            };
+            T x[kAB][4], xnx[kAB][4];
+            auto load = [&](T (&dst)[kAB][4], int c0, int nc) {
+#pragma unroll
+                for (int jb = 0; jb < kAB; ++jb)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) dst[jb][g] = buf_load<T>(rs, off(jb, g, c0, nc));
+            };
+            load(x, s0 * kASlab, min(kASlab, ncols - s0 * kASlab));
+            for (int slab = s0; slab < s1; ++slab) {
+                const int c0 = slab * kASlab;
+                const int nc = min(kASlab, ncols - c0);
+                if (slab + 1 < s1) load(xnx, c0 + kASlab, min(kASlab, ncols - c0 - kASlab));
+                v4 acc[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
+#pragma unroll
+                for (int jb = 0; jb < kAB; ++jb) {
+                    if (w + kAW * jb < nblk) {
+#pragma unroll
+                        for (int st = 0; st < 4; ++st)
+#pragma unroll
+                            for (int ab = 0; ab < 2; ++ab) acc[ab] = Mfma<T>::mma(Vw[jb][st][ab], x[jb][st], acc[ab]);
+                    }
+                }
+                reduce_w2(acc);
+#pragma unroll
+                for (int jb = 0; jb < kAB; ++jb) {
+                    if (w + kAW * jb < nblk) {
+                        v4 a = {x[jb][0], x[jb][1], x[jb][2], x[jb][3]};
+                        // W2 straight from LDS (no register copy: registers are
+                        // the limit of this path)
+#pragma unroll
+                        for (int st = 0; st < 8; ++st)
+                            if (st < ksteps) a = Mfma<T>::mma(Vu[jb][st], sW2[(4 * st + q) * 17 + l15], a);
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) buf_store<T>(a[g], rs, off(jb, g, c0, nc));
+                    }
+                }
+                if (slab + 1 < s1) {
+#pragma unroll
+                    for (int jb = 0; jb < kAB; ++jb)
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) x[jb][g] = xnx[jb][g];
+                }
+            }
+        }
+    } else {
+
     T xn[kXN];
     slab_load<T, TR>(base, ld, sMap, nr, s0 * kASlab, min(kASlab, ncols - s0 * kASlab), tid, xn);
     slab_to_lds<T, TR>(sX, nrp, tid, xn);
@@ -679,7 +807,7 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
         if (slab + 1 < s1)   // next slab in flight while this one computes
             slab_load<T, TR>(base, ld, sMap, nr, c0 + kASlab, min(kASlab, ncols - c0 - kASlab), tid, xn);
 
-        // ---- W = V^T X (32 x 16): partial over this wave's rows, ds_add ------
+        // ---- W = V^T X (32 x 16): partial over this wave's rows -------------
         {
             v4 acc[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
 #pragma unroll
@@ -694,36 +822,8 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
                     }
                 }
             }
-            if (w < nblk) {
-#pragma unroll
-                for (int ab = 0; ab < 2; ++ab)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) sWp[w][(ab * 16 + q + 4 * g) * 16 + l15] = acc[ab][g];
-            }
+            reduce_w2(acc);   // ---- W2 = -(T^T W) into sW2
         }
-        lds_barrier();
-        // cross-wave sum in wave order: the result does not depend on which
-        // wave finishes first (stage 1 is bitwise reproducible run to run)
-        {
-            const int nwp = min(kAW, nblk);
-            T s = sWp[0][tid];
-            for (int k = 1; k < nwp; ++k) s += sWp[k][tid];
-            sW[(tid >> 4) * 17 + (tid & 15)] = s;
-        }
-        lds_barrier();
-        // ---- W2 = -(T^T W) -------------------------------------------------
-        if (w < 2) {
-            const int ab = w;
-            v4 acc = {0, 0, 0, 0};
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const int k = 4 * s + q;
-                acc = Mfma<T>::mma(sT[k * 32 + ab * 16 + arw], sW[k * 17 + l15], acc);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g) sW2[(ab * 16 + q + 4 * g) * 17 + l15] = -acc[g];
-        }
-        lds_barrier();
         // ---- X += V W2 ----------------------------------------------------
         {
             T bw[8];
@@ -752,15 +852,16 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
             lds_barrier();
         }
     }
+    }   // LDS-staged path
 }
 
-template <typename T, bool TR>
+template <typename T, bool TR, bool DIRECT>
 __global__ void __launch_bounds__(kAT)
 k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
         const T *__restrict__ VTws, const T *__restrict__ Tws)
 {
     __shared__ ApplyLds<T> L;
-    apply_body<T, TR>(L, blockIdx.x, blockIdx.y, base, ld, la, ncols, spw, Vws, VTws, Tws);
+    apply_body<T, TR, DIRECT>(L, blockIdx.x, blockIdx.y, base, ld, la, ncols, spw, Vws, VTws, Tws);
 }
 
 // k_apply_factor: the apply of tree level l (blockIdx.y >= 1) and the factor
@@ -771,7 +872,7 @@ k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *_
 // the side stream and its two event hand-offs per panel side (about 6-7 us of
 // idle GPU each, measured).  Row y = 0 is dispatched first, so the factor
 // starts at once on a CU of its own.
-template <typename T, bool TR>
+template <typename T, bool TR, bool DIRECT>
 __global__ void __launch_bounds__(kAT)
 k_apply_factor(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
                const T *__restrict__ VTws, const T *__restrict__ Tws, T *__restrict__ fbase, long fld, LvArgs fa,
@@ -786,7 +887,7 @@ k_apply_factor(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, con
         if ((int)blockIdx.x < nfac) factor_body<T, TR>(L.f, blockIdx.x, fbase, fld, fa, fV, fVT, fT);
         return;
     }
-    apply_body<T, TR>(L.a, blockIdx.x, blockIdx.y - 1, base, ld, la, ncols, spw, Vws, VTws, Tws);
+    apply_body<T, TR, DIRECT>(L.a, blockIdx.x, blockIdx.y - 1, base, ld, la, ncols, spw, Vws, VTws, Tws);
 }
 
 // --------------------------------------------------------------------------
@@ -837,23 +938,37 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
     int spw = std::max(1, (groups * nslabs + tgt - 1) / tgt);
     while (spw < nslabs && (long)groups * ((nslabs + spw - 1) / spw) > tgt) ++spw;
     const T *V = (const T *)ws.V[level], *VT = (const T *)ws.VT[level], *Tm = (const T *)ws.T[level];
+    // Row-major view: the slab can stay in registers (apply_body's direct
+    // path).  Measured at N = 8192 (same box): fp32 stage 1 62.7 -> 61.5 ms;
+    // fp64 88.5 -> 102.5 ms (the fp64 tile needs more than the 256 VGPRs of a
+    // 2-waves-per-SIMD kernel and spills), so fp64 keeps the LDS-staged path.
+    // BRD_S1_DIRECT=0 / 1 overrides (tuning).
+    static const char *denv = getenv("BRD_S1_DIRECT");
+    const bool want = denv ? denv[0] == '1' : sizeof(T) == 4;
+    const int direct = !trans && want && (level == 0 || t.bk % 16 == 0) &&
+                               ((long)t.M * ld + ncols) * (long)sizeof(T) < (1L << 31) ? 1 : 0;
     if (fuse) {
         dim3 grid(groups, 1 + (nslabs + spw - 1) / spw), block(kAT);
         const LvArgs fa = lv_args(t, level + 1);
         T *fV = (T *)ws.V[level + 1], *fVT = (T *)ws.VT[level + 1], *fT = (T *)ws.T[level + 1];
         if (trans)
-            hipLaunchKernelGGL((k_apply_factor<T, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+            hipLaunchKernelGGL((k_apply_factor<T, true, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+                               fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+        else if (direct)
+            hipLaunchKernelGGL((k_apply_factor<T, false, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         else
-            hipLaunchKernelGGL((k_apply_factor<T, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+            hipLaunchKernelGGL((k_apply_factor<T, false, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         return hipGetLastError();
     }
     dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
     if (trans)
-        hipLaunchKernelGGL((k_apply<T, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+        hipLaunchKernelGGL((k_apply<T, true, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+    else if (direct)
+        hipLaunchKernelGGL((k_apply<T, false, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
     else
-        hipLaunchKernelGGL((k_apply<T, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+        hipLaunchKernelGGL((k_apply<T, false, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
     return hipGetLastError();
 }
 

@@ -42,7 +42,13 @@ for st in "$@"; do
     pmc)
       n=$(echo $arg | cut -d: -f1); dt=$(echo $arg | cut -d: -f2); bash tools/pmc.sh ${tag} ${n:-8192} ${dt:-f64} || exit 1 ;;
     s1)
-      timeout -k 10 300 python tools/s1time.py ${arg:-8192} s1 2>&1 | tail -1 || exit 1 ;;
+      # s1[:N[:VARS[:DT]]]: stage-1 timing per environment variant (';'-separated)
+      n=$(echo "$arg" | cut -d: -f1); vars=$(echo "$arg" | cut -s -d: -f2); dt=$(echo "$arg" | cut -s -d: -f3)
+      [ -z "$vars" ] && vars="BASE=1"
+      IFS=';' read -ra VS <<< "$vars"
+      for v in "${VS[@]}"; do
+        env $v timeout -k 5 200 python tools/s1time.py ${n:-8192} "$v" ${dt:-f64} 2>&1 | tail -1 || exit 1
+      done ;;
     s2)
       n=${arg%%:*}; vars=${arg#*:}; [ "$vars" = "$arg" ] && vars="BASE=1"
       rm -f /tmp/s2time_ref.npy

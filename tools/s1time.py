@@ -13,9 +13,10 @@ import svdsolver_amd as S  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 tag = sys.argv[2] if len(sys.argv) > 2 else "run"
+dt = torch.float32 if (len(sys.argv) > 3 and sys.argv[3] == "f32") else torch.float64
 b = 32
 g = torch.Generator(device="cuda").manual_seed(5)
-A0 = torch.rand(n, n, dtype=torch.float64, device="cuda", generator=g) * 5
+A0 = torch.rand(n, n, dtype=dt, device="cuda", generator=g) * 5
 ts = []
 for it in range(4):
     A = A0.clone()
@@ -24,8 +25,8 @@ for it in range(4):
     S.ge2band(A, b)
     torch.cuda.synchronize()
     ts.append((time.perf_counter() - t0) * 1e3)
-ref = "/tmp/s1time_ref.npy"
-dd = np.abs(torch.diagonal(A, 1).cpu().numpy())
+ref = f"/tmp/s1time_ref_{n}_{dt}.npy"
+dd = np.abs(torch.diagonal(A, 1).double().cpu().numpy())
 if not os.path.exists(ref):
     np.save(ref, dd)
     dev = 0.0

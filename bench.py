@@ -283,13 +283,21 @@ def maybe_spawn(args) -> None:
 def main():
     args = parse()
     if args.lanes is None:
-        args.lanes = 4 if ("WORLD_SIZE" not in os.environ and args.gpus <= 1) else 1
+        args.lanes = 4 if ("WORLD_SIZE" not in os.environ and args.gpus <= 1 and args.pipeline == "on") else 1
     # Every lane launches on two HIP streams; with the runtime's default of 4
     # hardware queues per process, streams beyond that share a queue and
     # their work serialises (measured: 2 lanes 14.1 -> 17.8 TFLOP/s once each
-    # stream has a queue).  Read when the HIP runtime initialises, so set first.
+    # stream has a queue).  Read when the HIP runtime initialises, so set first;
+    # raised (never lowered) from whatever the environment holds (4 on the
+    # MI355X pool, HIP's own default).
     if args.lanes > 1:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, 2 * args.lanes + 4)))
+        want = min(32, 2 * args.lanes + 4)
+        try:
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+        except ValueError:
+            have = 0
+        if have < want:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     maybe_spawn(args)
     import torch
     import torch.distributed as dist
@@ -395,10 +403,15 @@ def main():
 
     def issue(first, count, ev=None):
         last = None
+        # one reduction at a time: lane 0 only.  Matrices queued on the other
+        # lanes' streams would sit behind cross-stream barriers, and queues
+        # parked on barriers slow the dispatch of the active one (measured:
+        # stage 1 137 ms vs 89 ms with 4 lanes' streams waiting).
+        nl = lanes if mode["pipe"] else 1
         for i in range(count):
             j = first + i
             A = mats[j]
-            s_a, s_b = sa_l[j % lanes], sb_l[j % lanes]
+            s_a, s_b = sa_l[j % nl], sb_l[j % nl]
             with torch.cuda.stream(s_a):
                 if not mode["pipe"] and last is not None:
                     s_a.wait_event(last)
@@ -509,6 +522,7 @@ def main():
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
                                     if pipelined else "off: one reduction at a time"),
                        "stage2_cus": s2_cus or "all", "lanes": lanes,
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},
             "latency_ms_per_reduction": round(s1 + s2, 3),
             "one_at_a_time": one_at_a_time,

@@ -7,7 +7,7 @@
 #   tests            all -m gpu tests (pytest, per-test timeouts)
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     one bench.py line (ARGS: comma-separated extra flags, e.g. bench:--dtype,f32)
-#   prof[:N]         rocprofv3 --kernel-trace --stats of a short pipelined bench at N (default 8192)
+#   prof[:N:DT:ARGS] rocprofv3 --kernel-trace --stats of a short bench (default one reduction at a time)
 #   pmc[:N:DT]       FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh) at N, dtype DT
 #   s1[:N]           stage-1 timing (tools/s1time.py)
 #   s2[:N:VARS]      stage-2 timing per environment variant (VARS: ';'-separated, each 'K=V K2=V2')
@@ -34,11 +34,15 @@ for st in "$@"; do
         || { echo BENCH FAILED; tail -5 gpurun_out/b_${tag}_$k.log; exit 1; }
       grep metric gpurun_out/b_${tag}_$k.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('BENCH', d['value'], d['ms_per_step'], d['stage_ms'], d.get('one_at_a_time'), d['kernel_ms_per_step'], d['roofline']['frac'])" ;;
     prof)
-      n=${arg:-8192}
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${tag}_$n -o run -- \
-        python3 bench.py --n $n --steps 2 --warmup 1 --cpu-baseline off --one-at-a-time off > gpurun_out/p_${tag}_$n.log 2>&1 \
-        || { echo PROF FAILED; tail -5 gpurun_out/p_${tag}_$n.log; exit 1; }
-      f=$(find gpurun_out/prof_${tag}_$n -name "*kernel_stats.csv" | head -1); echo "stats: $f"; cut -c1-150 "$f" | head -10 ;;
+      # prof[:N[:DT[:ARGS]]]: default ARGS --pipeline,off (one reduction at a
+      # time: the pass bench.py's roofline durations come from)
+      n=$(echo "$arg" | cut -d: -f1); dt=$(echo "$arg" | cut -s -d: -f2); pa=$(echo "$arg" | cut -s -d: -f3)
+      n=${n:-8192}; dt=${dt:-f64}; pa=${pa:---pipeline,off}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${tag}_${n}_$dt -o run -- \
+        python3 bench.py --n $n --dtype $dt --steps 3 --warmup 1 --cpu-baseline off ${pa//,/ } > gpurun_out/p_${tag}_${n}_$dt.log 2>&1 \
+        || { echo PROF FAILED; tail -5 gpurun_out/p_${tag}_${n}_$dt.log; exit 1; }
+      grep metric gpurun_out/p_${tag}_${n}_$dt.log | cut -c1-400
+      f=$(find gpurun_out/prof_${tag}_${n}_$dt -name "*kernel_stats.csv" | head -1); echo "stats: $f"; cut -c1-150 "$f" | head -10 ;;
     pmc)
       n=$(echo $arg | cut -d: -f1); dt=$(echo $arg | cut -d: -f2); bash tools/pmc.sh ${tag} ${n:-8192} ${dt:-f64} || exit 1 ;;
     s1)

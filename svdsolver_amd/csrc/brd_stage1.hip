@@ -55,7 +55,23 @@ hipError_t read_stamps(unsigned long long *out) {
         if (blockIdx.x == 0 && threadIdx.x == 0)                                   \
             for (int k = 0; k < 5; ++k) g_stamps[10 + k] = ph_acc[k];              \
     } while (0)
+// per-phase cycle accumulators of the apply slab loop (wave 0 of workgroup (0,0))
+#define APH_DECL unsigned long long aph_t = __builtin_amdgcn_s_memtime(), aph_acc[6] = {0, 0, 0, 0, 0, 0}
+#define APH(k)                                                                     \
+    do {                                                                           \
+        const unsigned long long aph_n = __builtin_amdgcn_s_memtime();             \
+        aph_acc[k] += aph_n - aph_t;                                               \
+        aph_t = aph_n;                                                             \
+    } while (0)
+#define APH_STORE                                                                  \
+    do {                                                                           \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                \
+            for (int k = 0; k < 6; ++k) g_stamps[20 + k] = aph_acc[k];             \
+    } while (0)
 #else
+#define APH_DECL do {} while (0)
+#define APH(k) do {} while (0)
+#define APH_STORE do {} while (0)
 #define STAMP(k) do {} while (0)
 #define PH_DECL do {} while (0)
 #define PH(k) do {} while (0)
@@ -800,12 +816,14 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
     slab_load<T, TR>(base, ld, sMap, nr, s0 * kASlab, min(kASlab, ncols - s0 * kASlab), tid, xn);
     slab_to_lds<T, TR>(sX, nrp, tid, xn);
     __syncthreads();
+    APH_DECL;
 
     for (int slab = s0; slab < s1; ++slab) {
         const int c0 = slab * kASlab;
         const int nc = min(kASlab, ncols - c0);
         if (slab + 1 < s1)   // next slab in flight while this one computes
             slab_load<T, TR>(base, ld, sMap, nr, c0 + kASlab, min(kASlab, ncols - c0 - kASlab), tid, xn);
+        APH(0);
 
         // ---- W = V^T X (32 x 16): partial over this wave's rows -------------
         {
@@ -822,7 +840,9 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
                     }
                 }
             }
+            APH(1);
             reduce_w2(acc);   // ---- W2 = -(T^T W) into sW2
+            APH(2);
         }
         // ---- X += V W2 ----------------------------------------------------
         {
@@ -845,13 +865,17 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
             }
         }
         lds_barrier();
+        APH(3);
         slab_store<T, TR>(base, ld, sMap, nr, c0, nc, tid, sX);
         lds_barrier();
+        APH(4);
         if (slab + 1 < s1) {
             slab_to_lds<T, TR>(sX, nrp, tid, xn);
             lds_barrier();
         }
+        APH(5);
     }
+    APH_STORE;
     }   // LDS-staged path
 }
 

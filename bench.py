@@ -89,6 +89,9 @@ def parse():
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                    help="dist mode communicator: RCCL (one GPU per rank) or the host callback over gloo "
                         "(rehearsal of the multi-rank path with every rank on GPU 0)")
+    p.add_argument("--stages", choices=["12", "1", "2"], default="12",
+                   help="developer diagnostic: run only stage 1 or only stage 2 inside each step "
+                        "(the line is then labelled, and is not the metric)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the distributed path even at world size 1 (launch through torch.distributed.run)")
     return p.parse_args()
@@ -381,10 +384,12 @@ def main():
             mats.append(M)
 
         def stage1(A, j):
-            S.ge2band(A, b, sync=False)
+            if args.stages != "2":
+                S.ge2band(A, b, sync=False)
 
         def stage2(A, j):
-            S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
+            if args.stages != "1":
+                S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
     # Two launch streams: stage 1 (and the band gather) on s_a, stage 2 on s_b.
     # Pipelined, stage 2 of matrix i waits only for stage 1 of matrix i, so it
@@ -492,7 +497,7 @@ def main():
     value = matrices * args.steps * flops_per / elapsed / 1e9
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.stages == "12" else f"DIAGNOSTIC stage {args.stages} only (not the metric)",
             "value": round(value, 2),
             "unit": "GFLOP/s",
             "n_gpus": world,

@@ -821,8 +821,6 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
     for (int slab = s0; slab < s1; ++slab) {
         const int c0 = slab * kASlab;
         const int nc = min(kASlab, ncols - c0);
-        if (slab + 1 < s1)   // next slab in flight while this one computes
-            slab_load<T, TR>(base, ld, sMap, nr, c0 + kASlab, min(kASlab, ncols - c0 - kASlab), tid, xn);
         APH(0);
 
         // ---- W = V^T X (32 x 16): partial over this wave's rows -------------
@@ -840,9 +838,19 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
                     }
                 }
             }
+            // next slab in flight while this one finishes: issued after the W
+            // MFMAs, not before them, so that the previous slab's stores drain
+            // under those MFMAs instead of stalling the issue of these loads
+#ifndef BRD_PF_POS
+#define BRD_PF_POS 1
+#endif
+            if (BRD_PF_POS == 1 && slab + 1 < s1)
+                slab_load<T, TR>(base, ld, sMap, nr, c0 + kASlab, min(kASlab, ncols - c0 - kASlab), tid, xn);
             APH(1);
             reduce_w2(acc);   // ---- W2 = -(T^T W) into sW2
             APH(2);
+            if (BRD_PF_POS == 2 && slab + 1 < s1)
+                slab_load<T, TR>(base, ld, sMap, nr, c0 + kASlab, min(kASlab, ncols - c0 - kASlab), tid, xn);
         }
         // ---- X += V W2 ----------------------------------------------------
         {

@@ -685,6 +685,13 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
     const int arw = Mfma<T>::arow(lane);
 
     if (tid < nr) sMap[tid] = group_row(tid, grp, la);
+    // LDS-staged path: the run's first slab is in flight together with the V
+    // fragments below (one memory latency before the first slab, not two)
+    T xn[DIRECT ? 1 : kXN];
+    if constexpr (!DIRECT) {
+        lds_barrier();
+        slab_load<T, TR>(base, ld, sMap, nr, s0 * kASlab, min(kASlab, ncols - s0 * kASlab), tid, xn);
+    }
     for (int e = tid; e < 32 * 32; e += kAT) sT[e] = Tm[e];
 
     // ---- V fragments for this wave's row blocks (registers, whole run) -----
@@ -812,8 +819,6 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
         }
     } else {
 
-    T xn[kXN];
-    slab_load<T, TR>(base, ld, sMap, nr, s0 * kASlab, min(kASlab, ncols - s0 * kASlab), tid, xn);
     slab_to_lds<T, TR>(sX, nrp, tid, xn);
     __syncthreads();
     APH_DECL;

@@ -288,35 +288,47 @@ def overlap_cus(n: int) -> int:
     return 32 if n >= 1024 else 16
 
 
-def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = None, sync: bool = True):
+def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = None, sync: bool = True,
+                lanes: int = 1):
     """Two-stage reduction of a sequence of square CUDA tensors, each in place,
-    pipelined over two HIP streams: stage 2 of matrix i (its own stream,
-    ``s2_cus`` workgroups) runs beside stage 1 of matrix i+1 (the other
-    stream, sized for the remaining CUs).  Returns [(d, e)] per matrix (device
+    pipelined over pairs of HIP streams ("lanes"): on a lane, stage 2 of
+    matrix i (its own stream, ``s2_cus`` workgroups) runs beside stage 1 of the
+    lane's next matrix (the other stream, sized for the remaining CUs); matrix
+    i goes to lane i mod ``lanes``.  Returns [(d, e)] per matrix (device
     tensors).  Each matrix sees exactly the calls of ge2band + band2bd; only
     their overlap differs.  The library's overlap setting is restored on exit.
+    More than one lane pays only with one hardware queue per stream: set
+    GPU_MAX_HW_QUEUES >= 2 * lanes + 4 (at most 32) before HIP initialises
+    (DESIGN.md, "lanes").
     """
     import torch
     if not mats:
         return []
+    if lanes < 1:
+        raise ValueError("lanes must be >= 1")
     dev = mats[0].device
     cus = overlap_cus(mats[0].shape[0]) if s2_cus is None else int(s2_cus)
-    s_a, s_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    s_a.wait_stream(torch.cuda.current_stream(dev))
+    lanes = min(int(lanes), len(mats))
+    s_a = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    s_b = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    for s in s_a:
+        s.wait_stream(torch.cuda.current_stream(dev))
     out = []
     set_overlap(cus)
     try:
-        for A in mats:
-            with torch.cuda.stream(s_a):
+        for i, A in enumerate(mats):
+            sa, sb = s_a[i % lanes], s_b[i % lanes]
+            with torch.cuda.stream(sa):
                 ge2band(A, b, sync=False)
                 done1 = torch.cuda.Event()
-                done1.record(s_a)
-            with torch.cuda.stream(s_b):
-                s_b.wait_event(done1)
+                done1.record(sa)
+            with torch.cuda.stream(sb):
+                sb.wait_event(done1)
                 out.append(band2bd(A, b, sigma=sigma, sync=False))
     finally:
         set_overlap(0)
-    torch.cuda.current_stream(dev).wait_stream(s_b)
+    for s in s_b:
+        torch.cuda.current_stream(dev).wait_stream(s)
     if sync:
         torch.cuda.synchronize(dev)
         check_errors()

@@ -322,7 +322,8 @@ def test_cli_svd_runs(S):
     assert len(vals) == 5 and all(a >= b for a, b in zip(vals, vals[1:])) and vals[0] > 0
 
 
-def test_reduce_many_pipelined_matches_serial(S):
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_reduce_many_pipelined_matches_serial(S, lanes):
     """reduce_many: stage 2 of matrix i on its own stream (32 workgroups) beside
     stage 1 of matrix i+1 (the remaining CUs).  Every matrix gets the serial
     path's band bit for bit (the launch sizing under the overlap changes which
@@ -338,7 +339,7 @@ def test_reduce_many_pipelined_matches_serial(S):
         S.ge2band(dA, b)
         bands.append(np.abs(dA.cpu().numpy()))
     mats = [torch.from_numpy(A).cuda() for A in As]
-    got = S.reduce_many(mats, b, sigma=True)
+    got = S.reduce_many(mats, b, sigma=True, lanes=lanes)
     i, j = np.indices((n, n))
     inb = (j >= i) & (j - i <= b)
     for A, (d, e) in zip(As, got):

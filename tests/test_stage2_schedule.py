@@ -101,3 +101,41 @@ def exact_ring_need(n, b, S, sigma=False):
 def test_ring_size_formula_is_sufficient(n, b, S):
     assert ring_min_rows(b, S) >= exact_ring_need(n, b, S)
     assert ring_min_rows(b, S) >= exact_ring_need(n, b, S, sigma=True)
+
+
+def corner_rule_violations(n, b, sigma=False):
+    """A finer schedule than lag 3 (measured and not kept, DESIGN.md stage 2
+    round 2): window t of sweep i+1 starts once sweep i has finished window
+    t+2, and only its bottom-right corner's row (right window) or column (left
+    window) waits for window t+3.
+    Transitively, when window t of sweep i+d starts, sweep i has finished
+    windows up to t+3d-1, and when its corner part runs, up to t+3d.  Valid iff
+    every overlap with a later window of an earlier sweep is exactly that
+    corner element, at distance d = 1, and the corner is not in the window's
+    source row / column.  Returns the violating pairs."""
+    W = windows(n, n, b, sigma)
+    bad = []
+    for i in W:
+        for d in range(1, 2 * b + 6):
+            ip = i + d
+            if ip not in W:
+                break
+            for tp, wb in enumerate(W[ip]):
+                if wb is None:
+                    continue
+                right = tp % 2 == 0
+                corner = (wb[1] - 1, wb[1], wb[3] - 1, wb[3])
+                for t, wa in enumerate(W[i]):
+                    if wa is None or t < tp + 3 * d or not _overlap(wa, wb):
+                        continue
+                    inter = (max(wa[0], wb[0]), min(wa[1], wb[1]), max(wa[2], wb[2]), min(wa[3], wb[3]))
+                    src_ok = (wb[1] - 1 > wb[0]) if right else (wb[3] - 1 > wb[2])
+                    if not (d == 1 and t == tp + 3 and inter == corner and src_ok):
+                        bad.append((i, t, ip, tp))
+    return bad
+
+
+@pytest.mark.parametrize("sigma", [False, True])
+@pytest.mark.parametrize("n,b", [(300, 32), (257, 32), (130, 8), (100, 4), (50, 2), (40, 1), (333, 16)])
+def test_lag2_corner_rule_preserves_serial_order(n, b, sigma):
+    assert corner_rule_violations(n, b, sigma) == []

@@ -8,7 +8,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     one bench.py line (ARGS: comma-separated extra flags, e.g. bench:--dtype,f32)
 #   prof[:N:DT:ARGS] rocprofv3 --kernel-trace --stats of a short bench (default one reduction at a time)
-#   pmc[:N:DT]       FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh) at N, dtype DT
+#   pmc[:N:DT:ARGS]  FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh) at N, dtype DT (+ bench args)
 #   s1[:N]           stage-1 timing (tools/s1time.py)
 #   s2[:N:VARS]      stage-2 timing per environment variant (VARS: ';'-separated, each 'K=V K2=V2')
 #   py:FILE[:ARGS]   run a python file with comma-separated args
@@ -44,7 +44,7 @@ for st in "$@"; do
       grep metric gpurun_out/p_${tag}_${n}_$dt.log | cut -c1-400
       f=$(find gpurun_out/prof_${tag}_${n}_$dt -name "*kernel_stats.csv" | head -1); echo "stats: $f"; cut -c1-150 "$f" | head -10 ;;
     pmc)
-      n=$(echo $arg | cut -d: -f1); dt=$(echo $arg | cut -d: -f2); bash tools/pmc.sh ${tag} ${n:-8192} ${dt:-f64} || exit 1 ;;
+      n=$(echo $arg | cut -d: -f1); dt=$(echo $arg | cut -s -d: -f2); ex=$(echo $arg | cut -s -d: -f3); bash tools/pmc.sh ${tag} ${n:-8192} ${dt:-f64} "$ex" || exit 1 ;;
     s1)
       # s1[:N[:VARS[:DT]]]: stage-1 timing per environment variant (';'-separated)
       n=$(echo "$arg" | cut -d: -f1); vars=$(echo "$arg" | cut -s -d: -f2); dt=$(echo "$arg" | cut -s -d: -f3)

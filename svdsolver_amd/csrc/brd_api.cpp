@@ -121,6 +121,9 @@ struct Ctx {
     int *s2_err_host = nullptr;  // pinned copy of an error word
     int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
+    // events armed for the next launch (ProfScope in launch mode)
+    hipEvent_t ext_a = nullptr, ext_b = nullptr;
+    bool ext_armed = false, ext_taken = false;
     std::map<std::string, ProfAcc> acc;
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
@@ -262,25 +265,56 @@ static hipEvent_t get_event() {
     return e;
 }
 
+// Per-launch timing for brd_profile_*.  Default mode: events recorded on the
+// launch stream before and after the launch (they also take in the dispatch
+// gap).  Launch mode (the stage-1 apply, the roofline's kernel): the events
+// are handed to the launch itself (api_take_launch_events ->
+// hipExtLaunchKernel), which stamps the kernel's own start and end.
 struct ProfScope {
-    bool on;
+    bool on, launch_mode;
     Pending p;
     hipStream_t s;
-    ProfScope(const char *kind, double flops, double bytes, hipStream_t s_) : on(g_ctx.prof), s(s_) {
+    ProfScope(const char *kind, double flops, double bytes, hipStream_t s_, bool launch = false)
+        : on(g_ctx.prof), launch_mode(launch), s(s_) {
         if (!on) return;
         p.kind = kind;
         p.flops = flops;
         p.bytes = bytes;
         p.a = get_event();
         p.b = get_event();
-        hipEventRecord(p.a, s);
+        if (launch_mode) {
+            g_ctx.ext_a = p.a;
+            g_ctx.ext_b = p.b;
+            g_ctx.ext_armed = true;
+            g_ctx.ext_taken = false;
+        } else {
+            hipEventRecord(p.a, s);
+        }
     }
     ~ProfScope() {
         if (!on) return;
-        hipEventRecord(p.b, s);
+        if (launch_mode) {
+            const bool taken = g_ctx.ext_taken;
+            g_ctx.ext_armed = g_ctx.ext_taken = false;
+            if (!taken) {   // nothing was launched in the scope
+                g_ctx.event_pool.push_back(p.a);
+                g_ctx.event_pool.push_back(p.b);
+                return;
+            }
+        } else {
+            hipEventRecord(p.b, s);
+        }
         g_ctx.pending.push_back(p);
     }
 };
+
+bool api_take_launch_events(hipEvent_t *start, hipEvent_t *stop) {
+    if (!g_ctx.ext_armed || g_ctx.ext_taken) return false;
+    *start = g_ctx.ext_a;
+    *stop = g_ctx.ext_b;
+    g_ctx.ext_taken = true;
+    return true;
+}
 
 static void prof_drain() {
     for (auto &p : g_ctx.pending) {
@@ -357,7 +391,7 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
     if (ncols <= 0) return BRD_OK;
     for (int l = 0; l < t.nlevels; ++l) {
         const double rows = (double)tree_level_rows(t, l);
-        ProfScope ps("s1_apply", 4.0 * t.bk * rows * ncols, 2.0 * rows * ncols * sizeof(T), s);
+        ProfScope ps("s1_apply", 4.0 * t.bk * rows * ncols, 2.0 * rows * ncols * sizeof(T), s, true);
         HIP_TRY(launch_apply<T>(trans, X, lda, t, l, ncols, ws, s, api_apply_target(), fuse ? P : nullptr));
     }
     return BRD_OK;

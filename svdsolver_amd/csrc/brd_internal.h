@@ -73,6 +73,11 @@ hipStream_t api_stream();                          // the library stream
 int api_apply_target();                            // workgroups per stage-1 apply launch
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
+// Profiling with kernel-bracketing events: a ProfScope in "launch" mode arms a
+// pair of events that the NEXT stage-1 launch takes (hipExtLaunchKernel
+// records them at the dispatch's start and end, the timestamps rocprofv3
+// reports); false when nothing is armed.
+bool api_take_launch_events(hipEvent_t *start, hipEvent_t *stop);
 void api_lock();
 void api_unlock();
 // Stage-1 panel helpers shared with the single-GPU loop.

@@ -25,6 +25,8 @@
 // as a left update of the transpose).  See DESIGN.md "Stage 1".
 #include "brd_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -956,6 +958,17 @@ hipError_t launch_factor(bool trans, T *base, long ld, const Tree &t, int level,
     return hipGetLastError();
 }
 
+// One kernel launch; with profiling armed (api_take_launch_events) the launch
+// itself stamps the profiler's events at the kernel's start and end.
+template <typename F, typename... Args>
+static void launch_timed(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    hipEvent_t ea, eb;
+    if (api_take_launch_events(&ea, &eb))
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ea, eb, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
+
 template <typename T>
 hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, int ncols,
                         const TreeWs &ws, hipStream_t s, int target, T *fuse_panel, long fuse_ld)
@@ -989,23 +1002,23 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
         const LvArgs fa = lv_args(t, level + 1);
         T *fV = (T *)ws.V[level + 1], *fVT = (T *)ws.VT[level + 1], *fT = (T *)ws.T[level + 1];
         if (trans)
-            hipLaunchKernelGGL((k_apply_factor<T, true, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+            launch_timed((k_apply_factor<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         else if (direct)
-            hipLaunchKernelGGL((k_apply_factor<T, false, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+            launch_timed((k_apply_factor<T, false, true>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         else
-            hipLaunchKernelGGL((k_apply_factor<T, false, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm,
+            launch_timed((k_apply_factor<T, false, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         return hipGetLastError();
     }
     dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
     if (trans)
-        hipLaunchKernelGGL((k_apply<T, true, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+        launch_timed((k_apply<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
     else if (direct)
-        hipLaunchKernelGGL((k_apply<T, false, true>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+        launch_timed((k_apply<T, false, true>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
     else
-        hipLaunchKernelGGL((k_apply<T, false, false>), grid, block, 0, s, base, ld, a, ncols, spw, V, VT, Tm);
+        launch_timed((k_apply<T, false, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
     return hipGetLastError();
 }
 

@@ -24,21 +24,24 @@ its own matrices (weak scaling).  The step time is the max over ranks and
 `value` is the whole-job GFLOP/s.
 
 What `value` measures (config.value_kind): the throughput of a STREAM of
-independent reductions -- K matrices issued back to back, stage 2 of matrix
-i on its own HIP stream beside stage 1 of matrix i+1 (`--pipeline on`, the
-default).  The same K steps one reduction at a time (the reference's
-per-instance timing, timing.h:79-82) are reported as `one_at_a_time`, and
-`latency_ms_per_reduction` is one matrix's stage 1 + stage 2 under overlap.
-After every timed region the library's sticky stage-2 error words are read
-(brd_check_errors): a stalled sweep fails the run instead of being timed.
+independent reductions -- K matrices (default 20) issued back to back on 4
+lanes of HIP stream pairs (one GPU; matrix j on lane j mod 4, stage 2 of a
+lane's matrix beside stage 1 of its next one; `--pipeline on`, the default),
+fill and drain inside the timed region.  The same K steps one reduction at a
+time on one lane (the reference's per-instance timing, timing.h:79-82) are
+reported as `one_at_a_time`, and `latency_ms_per_reduction` is one matrix's
+stage 1 + stage 2 under overlap.  After every timed region the library's
+sticky stage-2 error words are read (brd_check_errors): a stalled sweep
+fails the run instead of being timed.
 
 Rank 0 prints ONE JSON line.  `value` comes from K timed steps with no
-per-launch instrumentation; the same K steps are then run again with the
-library's HIP events around every launch (on the stream each kernel is
-launched on) for the dominant kernel's roofline object.  Also the CPU
-baseline: the reference's own tiled algorithm (built from its sources by
-oracle/Makefile) timed on this host at N = 320, 640, 1024 (about 10-20 s),
-with a c N^3 fit extrapolated to the GPU problem size (labelled as such).
+per-launch instrumentation; K more steps one at a time are then run with the
+library's per-launch events (for the stage-1 apply stamped by the launch
+itself, hipExtLaunchKernel) for the dominant kernel's roofline object.  Also
+the CPU baseline: the reference's own tiled algorithm (built from its
+sources by oracle/Makefile) timed on this host at N = 320, 640, 1024 (about
+10-20 s), with a c N^3 fit extrapolated to the GPU problem size (labelled as
+such).
 """
 from __future__ import annotations
 
@@ -60,8 +63,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n", type=int, default=None,
                    help="matrix size (default 8192 on one GPU, BASELINE configs[2]; 16384 across GPUs, configs[4])")
     p.add_argument("--dtype", choices=["f64", "f32"], default="f64")

@@ -65,7 +65,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--n", type=int, default=None,
+    # --size is the spelling to use under torch.distributed.run, whose own
+    # parser takes "--n" for an ambiguous abbreviation of its options
+    p.add_argument("--size", "--n", dest="n", type=int, default=None,
                    help="matrix size (default 8192 on one GPU, BASELINE configs[2]; 16384 across GPUs, configs[4])")
     p.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     p.add_argument("--band", type=int, default=32)
@@ -262,6 +264,15 @@ def free_port() -> int:
         return sk.getsockname()[1]
 
 
+def torchrun_cmd(gpus: int, argv, port: int) -> list:
+    """The torch.distributed.run command that re-runs this script on `gpus`
+    ranks with the same arguments ("--n" spelled "--size": the launcher's own
+    parser reads "--n" as an ambiguous abbreviation of its options)."""
+    fwd = ["--size" + a[3:] if a == "--n" or a.startswith("--n=") else a for a in argv]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + fwd
+
+
 def maybe_spawn(args) -> None:
     """`python bench.py --gpus N` with no launcher around it: start the N ranks
     as a torch.distributed.run child (one process per GPU, rendezvous on
@@ -281,8 +292,7 @@ def maybe_spawn(args) -> None:
         sys.exit(f"bench.py: --gpus {args.gpus} requested but only {ndev} GPU(s) are visible")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    cmd = torchrun_cmd(args.gpus, sys.argv[1:], free_port())
     sys.exit(subprocess.call(cmd, env=env))
 
 

@@ -24,3 +24,18 @@ def test_bench_rejects_world_size_mismatch():
                          capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode != 0
     assert "WORLD_SIZE=2" in out.stderr
+
+
+def test_torchrun_command_passes_size_through():
+    """`python bench.py --gpus N --n 16384`: the spawned torch.distributed.run
+    must hand every bench argument to the script (its own parser would take
+    "--n" as an ambiguous abbreviation of --nnodes / --nproc-per-node ...)."""
+    import importlib.util
+    from torch.distributed.run import get_args_parser
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cmd = bench.torchrun_cmd(2, ["--gpus", "2", "--n", "4096", "--steps", "3", "--warmup", "1"], 29999)
+    ns = get_args_parser().parse_args(cmd[3:])
+    assert ns.nproc_per_node == "2" and ns.training_script.endswith("bench.py")
+    assert ns.training_script_args == ["--gpus", "2", "--size", "4096", "--steps", "3", "--warmup", "1"]

@@ -527,11 +527,15 @@ def main():
                                    + f", band {b}, "
                                    + ("stage 2 = reference window geometry (compat)" if args.s2 == "compat"
                                       else "stage 2 = sigma-preserving geometry (BRD_SIGMA)"),
-                       "value_kind": (f"stream throughput: K independent matrices issued back to back on {lanes} "
-                                      "lane(s) of HIP streams (matrix j on lane j mod lanes; per lane stage 2 of "
-                                      "matrix i beside stage 1 of the next), fill and drain inside the timed region; "
-                                      "per-reduction latency under overlap: latency_ms_per_reduction; one reduction "
-                                      "at a time: one_at_a_time" if pipelined else "one reduction at a time"),
+                       "value_kind": (("stream throughput: K independent matrices issued back to back, each one's "
+                                       f"stage 1 sharded over the {world} ranks, its band gathered on rank j mod "
+                                       f"{world}, whose stage 2 runs beside the following matrices' stage 1; fill "
+                                       "and drain inside the timed region" if dist_mode else
+                                       f"stream throughput: K independent matrices issued back to back on {lanes} "
+                                       "lane(s) of HIP streams (matrix j on lane j mod lanes; per lane stage 2 of "
+                                       "matrix i beside stage 1 of the next), fill and drain inside the timed region; "
+                                       "per-reduction latency under overlap: latency_ms_per_reduction; one reduction "
+                                       "at a time: one_at_a_time") if pipelined else "one reduction at a time"),
                        "n": n, "band": b, "global_batch": matrices,
                        "matrices_per_timed_region": matrices * args.steps,
                        "parallelism": (f"stage1 block-cyclic columns over {world} GPUs ({'RCCL' if args.comm == 'rccl' else 'host gloo'}), stage2 on rank "

@@ -87,8 +87,8 @@ def parse():
     p.add_argument("--one-at-a-time", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: also time K steps without the overlap (reported as one_at_a_time)")
     p.add_argument("--lanes", type=int, default=None,
-                   help="pipelined, one GPU: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
-                        "(default 4; 1 across GPUs)")
+                   help="pipelined: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
+                        "(default 4; across GPUs each lane has its own RCCL communicator)")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -299,7 +299,7 @@ def maybe_spawn(args) -> None:
 def main():
     args = parse()
     if args.lanes is None:
-        args.lanes = 4 if ("WORLD_SIZE" not in os.environ and args.gpus <= 1 and args.pipeline == "on") else 1
+        args.lanes = 4 if args.pipeline == "on" else 1
     # Every lane launches on two HIP streams; with the runtime's default of 4
     # hardware queues per process, streams beyond that share a queue and
     # their work serialises (measured: 2 lanes 14.1 -> 17.8 TFLOP/s once each
@@ -353,41 +353,59 @@ def main():
     S.set_overlap(s2_cus)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
+    # Two launch streams per lane: stage 1 (and the band gather) on s_a, stage 2
+    # on s_b.  Pipelined, stage 2 of matrix i waits only for stage 1 of matrix
+    # i, so it runs beside stage 1 of the lane's next matrix (stage 2 is a
+    # latency-bound chain on a few dozen CUs, stage 1 HBM-bound on the rest);
+    # otherwise s_b's work is ordered after all of s_a's and vice versa (one
+    # reduction at a time).  L lanes side by side (default 4), matrix j on lane
+    # j mod L (the library keeps a workspace -- and, across GPUs, an RCCL
+    # communicator -- per launch stream), so one lane's latency-bound work
+    # (leaf factors, tail panels, the stage-2 chase, the distributed panel
+    # loop's collectives) overlaps another lane's HBM-bound trailing updates.
+    # Measured at N = 8192 fp64 (20 steps, one hardware queue per stream):
+    # L = 1 14.1 TFLOP/s, L = 2 18.2, L = 4 19.9, L = 8 20.3.
+    lanes = args.lanes if pipelined else 1
+    sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
     if dist_mode:
         from svdsolver_amd import dist as D
-        if args.comm == "host":
-            D.init_host()
-        else:
-            D.init_rccl()
+        for s_a in sa_l:   # one communicator per lane's stage-1 stream
+            if args.comm == "host":
+                D.init_host(stream=s_a)
+            else:
+                D.init_rccl(stream=s_a)
         n_loc = D.local_cols(n, b, world, rank)
         base = torch.rand((n, max(n_loc, 1)), dtype=tdt, device=dev, generator=g)[:, :n_loc] * 5.0
         mats = [base.contiguous().clone() for _ in range(nmat)]
         # Matrix j's band goes to rank j mod world, which runs its stage 2; two
-        # band buffers per rank so a gather never lands in a band whose sweep
-        # may still be running (the stage-1 stream also waits for that sweep).
-        Bfull = [torch.empty((n, n), dtype=tdt, device=dev) for _ in range(2 if pipelined else 1)]
-        s2_done = [None] * len(Bfull)
+        # band buffers per lane and rank so a gather never lands in a band whose
+        # sweep may still be running (the stage-1 stream also waits for that
+        # sweep).
+        nbuf = 2 if pipelined else 1
+        Bfull = [[torch.empty((n, n), dtype=tdt, device=dev) for _ in range(nbuf)] for _ in range(lanes)]
+        s2_done = [[None] * nbuf for _ in range(lanes)]
 
         def root_of(j):
             return j % world if pipelined else 0
 
         def band_of(j):
-            return (j // world) % len(Bfull)
+            return j % lanes, (j // lanes) % nbuf
 
         def stage1(A, j):
             D.ge2band(A, n, b, sync=False)
-            r, k = root_of(j), band_of(j)
-            if rank == r and s2_done[k] is not None:
-                torch.cuda.current_stream(dev).wait_event(s2_done[k])
-            D.gather_band(A, n, b, root=r, out=Bfull[k] if rank == r else None, sync=False)
+            r, (ln, k) = root_of(j), band_of(j)
+            if rank == r and s2_done[ln][k] is not None:
+                torch.cuda.current_stream(dev).wait_event(s2_done[ln][k])
+            D.gather_band(A, n, b, root=r, out=Bfull[ln][k] if rank == r else None, sync=False)
 
         def stage2(A, j):
             if rank == root_of(j):
-                k = band_of(j)
-                S.band2bd(Bfull[k], b, sigma=args.s2 == "sigma", sync=False, extract=False)
+                ln, k = band_of(j)
+                S.band2bd(Bfull[ln][k], b, sigma=args.s2 == "sigma", sync=False, extract=False)
                 e = torch.cuda.Event()
                 e.record(torch.cuda.current_stream(dev))
-                s2_done[k] = e
+                s2_done[ln][k] = e
     else:
         base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
         mats = []
@@ -404,20 +422,6 @@ def main():
             if args.stages != "1":
                 S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
-    # Two launch streams: stage 1 (and the band gather) on s_a, stage 2 on s_b.
-    # Pipelined, stage 2 of matrix i waits only for stage 1 of matrix i, so it
-    # runs beside stage 1 of matrix i+1 (stage 2 is a latency-bound chain on a
-    # few dozen CUs, stage 1 HBM-bound on the rest); otherwise s_b's work is
-    # ordered after all of s_a's and vice versa (one reduction at a time).
-    # --lanes L > 1 (one GPU): L such pipelines side by side, matrix j on lane
-    # j mod L (the library keeps a workspace per launch stream), so one lane's
-    # latency-bound tail panels and stage-2 chase overlap another lane's
-    # HBM-bound trailing updates.  Measured at N = 8192 fp64 (20 steps, one
-    # hardware queue per stream): L = 1 14.1 TFLOP/s, L = 2 18.2, L = 4 19.9,
-    # L = 8 20.3 -- default 4 (memory: warmup + 2K matrices resident).
-    lanes = args.lanes if (pipelined and not dist_mode) else 1
-    sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
-    sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
 
     def issue(first, count, ev=None):
         last = None

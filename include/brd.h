@@ -116,7 +116,13 @@ int brd_profile_query(const char *kernel, long long *launches, double *total_ms,
  * Collectives go to RCCL over xGMI (brd_dist_init, with an id from
  * brd_dist_unique_id on one rank, shared out of band) or to a host callback
  * (brd_dist_init_host: the library drains its stream, then calls fn, which
- * must complete the collective on the device buffers before returning). */
+ * must complete the collective on the device buffers before returning).
+ * A communicator belongs to the library stream current at its init
+ * (brd_set_stream); the first one is also the default for streams without
+ * their own.  Calls on a stream use that stream's communicator and a
+ * workspace of that stream, so several matrices' distributed reductions can
+ * run at once, one stream (and communicator) each; every rank must issue a
+ * communicator's calls in the same order.  brd_dist_finalize releases all. */
 enum brd_coll_op {
     BRD_COLL_BCAST = 0,         /* recv (== send) broadcast from root, count elems */
     BRD_COLL_ALLGATHER = 1,     /* send: count elems; recv: count * nranks elems    */

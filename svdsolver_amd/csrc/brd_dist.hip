@@ -33,8 +33,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace brd {
 
@@ -197,7 +199,30 @@ struct HostComm : Comm {
     }
 };
 
-std::unique_ptr<Comm> g_comm;
+// Communicators per launch stream.  brd_dist_init / brd_dist_init_host
+// register the new communicator for the library's current stream; the first
+// one is also the default for streams without a communicator of their own.
+// Several streams with their own communicators (and workspaces) let several
+// matrices' distributed panel loops run at once: the collectives of one
+// communicator are issued in the same order on every rank, those of different
+// communicators are independent.
+struct CommReg {
+    std::vector<std::pair<hipStream_t, std::unique_ptr<Comm>>> v;
+    Comm *find(hipStream_t s) const {
+        for (auto &e : v)
+            if (e.first == s) return e.second.get();
+        return v.empty() ? nullptr : v.front().second.get();
+    }
+    void add(hipStream_t s, std::unique_ptr<Comm> c) {
+        for (auto &e : v)
+            if (e.first == s) {
+                e.second = std::move(c);
+                return;
+            }
+        v.emplace_back(s, std::move(c));
+    }
+};
+CommReg g_comms;
 
 // ==========================================================================
 // layout helpers
@@ -235,7 +260,9 @@ struct DistWs {
         return BRD_OK;
     }
 };
-DistWs g_dws;
+// distributed workspaces per launch stream (std::map: nodes stay put)
+std::map<hipStream_t, DistWs> g_dws_by_stream;
+DistWs &dist_ws(hipStream_t s) { return g_dws_by_stream[s]; }
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -261,7 +288,8 @@ int dtype_of() { return sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32; }
 // ==========================================================================
 template <typename T>
 int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
-    Comm &C = *g_comm;
+    Comm &C = *g_comms.find(s);
+    DistWs &g_dws = dist_ws(s);
     const int P = C.nranks, me = C.rank;
     const int n_loc = local_cols(n, b, P, me);
     if (lda < std::max(n_loc, 1)) return api_fail(BRD_EINVAL, "lda_loc smaller than the local column count");
@@ -385,7 +413,8 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
 
 template <typename T>
 int gather_band(const T *A, int m, int n, int lda, int b, T *B, int ldb, int root, hipStream_t s) {
-    Comm &C = *g_comm;
+    Comm &C = *g_comms.find(s);
+    DistWs &g_dws = dist_ws(s);
     const int P = C.nranks, me = C.rank;
     const int np = npanels(n, b), npl = (np + P - 1) / P;
     const size_t per = 2 * (size_t)b * b, sz = sizeof(T);
@@ -414,12 +443,13 @@ struct Lock {
 template <typename T>
 int ge2band_dist_entry(T *A, int m, int n, int lda, int b, unsigned flags) {
     Lock lk;
-    if (!g_comm) return api_fail(BRD_EINVAL, "brd_dist_init / brd_dist_init_host has not been called");
-    if (!A && local_cols(n, b, g_comm->nranks, g_comm->rank) > 0) return api_fail(BRD_EINVAL, "A_loc is NULL");
+    hipStream_t s = api_stream();
+    const Comm *c = g_comms.find(s);
+    if (!c) return api_fail(BRD_EINVAL, "brd_dist_init / brd_dist_init_host has not been called");
+    if (!A && local_cols(n, b, c->nranks, c->rank) > 0) return api_fail(BRD_EINVAL, "A_loc is NULL");
     if (n < 1 || m < n) return api_fail(BRD_EINVAL, "need m >= n >= 1");
     if (b < 1 || b > kBmax) return api_fail(BRD_EINVAL, "band width outside [1, 32]");
     if (!(flags & BRD_DEVICE_PTR)) return api_fail(BRD_EINVAL, "distributed stage 1 takes device pointers (BRD_DEVICE_PTR)");
-    hipStream_t s = api_stream();
     int rc = ge2band_dist<T>(A, m, n, lda, b, s);
     if (rc == BRD_OK && !(flags & BRD_ASYNC)) D_HIP(hipStreamSynchronize(s));
     return rc;
@@ -428,11 +458,12 @@ int ge2band_dist_entry(T *A, int m, int n, int lda, int b, unsigned flags) {
 template <typename T>
 int gather_band_entry(const T *A, int m, int n, int lda, int b, T *B, int ldb, int root, unsigned flags) {
     Lock lk;
-    if (!g_comm) return api_fail(BRD_EINVAL, "brd_dist_init / brd_dist_init_host has not been called");
-    if (b < 1 || b > kBmax || n < 1 || m < n) return api_fail(BRD_EINVAL, "bad sizes");
-    if (root < 0 || root >= g_comm->nranks) return api_fail(BRD_EINVAL, "bad root rank");
-    if (g_comm->rank == root && (!B || ldb < n)) return api_fail(BRD_EINVAL, "root needs B with ldb >= n");
     hipStream_t s = api_stream();
+    const Comm *c = g_comms.find(s);
+    if (!c) return api_fail(BRD_EINVAL, "brd_dist_init / brd_dist_init_host has not been called");
+    if (b < 1 || b > kBmax || n < 1 || m < n) return api_fail(BRD_EINVAL, "bad sizes");
+    if (root < 0 || root >= c->nranks) return api_fail(BRD_EINVAL, "bad root rank");
+    if (c->rank == root && (!B || ldb < n)) return api_fail(BRD_EINVAL, "root needs B with ldb >= n");
     int rc = gather_band<T>(A, m, n, lda, b, B, ldb, root, s);
     if (rc == BRD_OK && !(flags & BRD_ASYNC)) D_HIP(hipStreamSynchronize(s));
     return rc;
@@ -466,7 +497,7 @@ int brd_dist_init(int rank, int nranks, const void *id, int id_bytes) {
     if (r != ncclSuccess) return brd::rccl_fail(r, "ncclCommInitRank");
     c->rank = rank;
     c->nranks = nranks;
-    brd::g_comm = std::move(c);
+    brd::g_comms.add(brd::api_stream(), std::move(c));
     return BRD_OK;
 }
 
@@ -479,13 +510,14 @@ int brd_dist_init_host(int rank, int nranks, brd_coll_fn fn, void *user) {
     c->user = user;
     c->rank = rank;
     c->nranks = nranks;
-    brd::g_comm = std::move(c);
+    brd::g_comms.add(brd::api_stream(), std::move(c));
     return BRD_OK;
 }
 
 int brd_dist_finalize(void) {
     brd::Lock lk;
-    brd::g_comm.reset();
+    brd::g_comms.v.clear();
+    brd::g_dws_by_stream.clear();
     return BRD_OK;
 }
 

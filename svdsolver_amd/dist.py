@@ -77,10 +77,19 @@ def unshard(shards: List, n: int, b: int):
 # ---------------------------------------------------------------------------
 # communicators
 # ---------------------------------------------------------------------------
-def init_rccl(group=None) -> None:
+def _bind(stream) -> None:
+    if stream is not None:
+        _check("brd_set_stream", lib.brd_set_stream(ctypes.c_void_p(stream.cuda_stream)))
+
+
+def init_rccl(group=None, stream=None) -> None:
     """RCCL communicator over the processes of ``group`` (torch.distributed
-    must be initialised; each process has selected its GPU)."""
+    must be initialised; each process has selected its GPU).  With ``stream``
+    (a torch CUDA stream) the communicator serves the calls made on that
+    stream only (one communicator per stream lets several matrices' reductions
+    run at once); the first communicator is also the default."""
     import torch.distributed as dist
+    _bind(stream)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     buf = ctypes.create_string_buffer(128)
     obj = [None]
@@ -103,12 +112,14 @@ class _DevArray:
 _TYPESTR = {DT_BYTE: "|u1", DT_F32: "<f4", DT_F64: "<f8"}
 
 
-def init_host(group=None) -> None:
+def init_host(group=None, stream=None) -> None:
     """Host-callback communicator: the library drains its stream and calls
     back; the collective runs through ``torch.distributed`` on host copies of
-    the device buffers (works with gloo, several ranks per GPU)."""
+    the device buffers (works with gloo, several ranks per GPU).  ``stream``:
+    as in :func:`init_rccl`."""
     import torch
     import torch.distributed as dist
+    _bind(stream)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
 
     def dev(ptr, count, dtype):

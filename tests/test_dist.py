@@ -176,3 +176,52 @@ def test_distributed_gather_band_to_last_rank(tmp_path):
     ref = S.brd_p1(A, b)
     assert _band_err(band, ref, b) <= 1e-12
     assert np.all(band[~_band_mask(n, b)] == 0)
+
+
+def _gpu_lanes_worker(rank, world, port, n, b, mode, lanes, out_path):
+    """One communicator per stream (brd_dist_init binds it to the library's
+    current stream): `lanes` matrices reduced at once, each on its own stream
+    with its own communicator and workspace."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
+    import torch.distributed as tdist
+    from svdsolver_amd import dist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    streams = [torch.cuda.Stream() for _ in range(lanes)]
+    for s in streams:
+        if mode == "rccl":
+            dist.init_rccl(stream=s)
+        else:
+            dist.init_host(stream=s)
+    locs, outs = [], []
+    for k, s in enumerate(streams):
+        A = np.random.default_rng(10 + k).uniform(1, 5, (n, n))
+        loc = torch.from_numpy(dist.shard(A, b, world, rank)).cuda()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            dist.ge2band(loc, n, b, sync=False)
+            outs.append(dist.gather_band(loc, n, b, root=0, sync=False))
+        locs.append(loc)
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.save(out_path, np.stack([B.cpu().numpy() for B in outs]))
+    dist.finalize()
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,mode,lanes", [(1, "rccl", 3), (2, "host", 2)])
+def test_distributed_stage1_streams_with_own_communicators(world, mode, lanes, tmp_path):
+    import torch.multiprocessing as mp
+    import svdsolver_amd as S
+    out = str(tmp_path / "bands.npy")
+    n, b = 512, 32
+    mp.spawn(_gpu_lanes_worker, args=(world, _free_port(), n, b, mode, lanes, out), nprocs=world, join=True)
+    bands = np.load(out)
+    for k in range(lanes):
+        A = np.random.default_rng(10 + k).uniform(1, 5, (n, n))
+        ref = S.brd_p1(A, b)
+        assert _band_err(bands[k], ref, b) <= 1e-12, k
+        assert np.all(bands[k][~_band_mask(n, b)] == 0)

@@ -30,7 +30,7 @@ int main(int argc, char **argv) {
         printf("stage2 n=%d: %.2f ms\n", n, ms);
         check_err("stage2");
     }
-    const int S = 2, nb = std::min(4096, (n - 1 + S - 1) / S);
+    const int S = argc > 2 ? atoi(argv[2]) : 3, nb = std::min(4096, (n - 1 + S - 1) / S);   // sweeps per bundle of the run
     std::vector<unsigned long long> st((size_t)nb * 6);
     (void)brd::read_s2stamps(st.data(), st.size());
     printf("beta   lead_t0   lead_done  trail_done  writer  loader   (cycles after the bundle's start)\n");

@@ -62,7 +62,7 @@ int brd_ge2band_f32(float *A, int m, int n, int lda, int b, int ngpus, unsigned 
 /* Stage 2: n x n band (bandwidth b) -> bidiagonal, in place, with the
  * reference's window geometry (BRD_COMPAT) or the sigma-preserving one
  * (BRD_SIGMA).  d (n) and e (n-1) receive the diagonal and super-diagonal
- * (same memory kind as A). */
+ * (same memory kind as A; e may be NULL when n = 1). */
 int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsigned flags);
 int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags);
 

@@ -499,11 +499,19 @@ template <typename T>
 static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     if (!A) return fail(BRD_EINVAL, "A is NULL");
-    if (n < 2) return fail(BRD_EINVAL, "need n >= 2 (n=%d)", n);
+    if (n < 1) return fail(BRD_EINVAL, "need n >= 1 (n=%d)", n);
     if (lda < n) return fail(BRD_EINVAL, "lda (%d) < n (%d)", lda, n);
     if (b < 1 || b > kBmax) return fail(BRD_EINVAL, "band width b=%d outside [1,%d]", b, kBmax);
     const bool extract = !(flags & BRD_NO_EXTRACT);
-    if (extract && (!dd || !ee)) return fail(BRD_EINVAL, "d/e are NULL (pass BRD_NO_EXTRACT to skip them)");
+    if (extract && !dd) return fail(BRD_EINVAL, "d is NULL (pass BRD_NO_EXTRACT to skip d and e)");
+    if (extract && !ee && n > 1) return fail(BRD_EINVAL, "e is NULL (pass BRD_NO_EXTRACT to skip d and e)");
+    if (n == 1) {   // a 1 x 1 band is its own bidiagonal (the reference's sweep loop runs zero times)
+        if (!extract) return BRD_OK;
+        const hipMemcpyKind k = (flags & BRD_DEVICE_PTR) ? hipMemcpyDeviceToDevice : hipMemcpyHostToHost;
+        HIP_TRY(hipMemcpyAsync(dd, A, sizeof(T), k, stream()));
+        if (!(flags & BRD_ASYNC) || !(flags & BRD_DEVICE_PTR)) HIP_TRY(hipStreamSynchronize(stream()));
+        return BRD_OK;
+    }
     const bool exact = (flags & BRD_EXACT_ORDER) != 0;
     const bool sigma = (flags & BRD_SIGMA) != 0;
     hipStream_t s = stream();

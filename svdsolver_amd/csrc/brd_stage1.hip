@@ -243,6 +243,8 @@ __device__ __forceinline__ float readlane(float v, int l) {
 //     for c > j, and records v_c^T v_j = w_c / u1_c for c < j (the T factor);
 //   * the owner of column j+1 forms its reflector (norm by a butterfly sum)
 //     and publishes it; one barrier.
+// The row-major view's tile is read (and its R written back) through LDS
+// staging, 256-byte rows at a time.
 // Columns stay unscaled ("raw") while the panel is factored: v_j =
 // X[:,j] / u1_j below the diagonal.  The j loop is unrolled by 4 so that the
 // owner's column index is static (no register-array indexing).
@@ -278,6 +280,7 @@ struct FactorLds {
     T sU1[32], sTau[32];   // 1/u1 and tau per column
     int sMap[kRmax];
     T sStage[kRmax / 2][33];   // row-major <-> register-layout staging, half a node at a time
+    T sX0[kRmax][5];           // wave 0's columns for the output (pitch 5: conflict-free)
 };
 
 // The factor of node grp (k_factor, or the factor role of k_apply_factor).
@@ -313,14 +316,41 @@ __device__ __forceinline__ void factor_body(FactorLds<T> &L, const int grp, T *_
     // ---- the tile into registers: x[k][cc] = X[lane + 64k][4w + cc] ----------
     STAMP(1);
     T x[kFR][4];
+    if constexpr (TR) {
+        // column-major view: lanes -> consecutive rows of one column (coalesced)
 #pragma unroll
-    for (int k = 0; k < kFR; ++k) {
-        const int i = lane + 64 * k;
-        const int pr = i < nr ? sMap[i] : 0;
+        for (int k = 0; k < kFR; ++k) {
+            const int i = lane + 64 * k;
+            const int pr = i < nr ? sMap[i] : 0;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = 4 * w + cc;
-            x[k][cc] = (i < nr && c < bk) ? *vptr<TR>(base, ld, pr, c) : (T)0;
+            for (int cc = 0; cc < 4; ++cc) {
+                const int c = 4 * w + cc;
+                x[k][cc] = (i < nr && c < bk) ? *vptr<TR>(base, ld, pr, c) : (T)0;
+            }
+        }
+    } else {
+        // row-major view: the register layout would touch 64 rows per load
+        // instruction; instead 32 threads read one 256-byte row (all 32 rows
+        // of a thread in flight at once) and the tile is redistributed through
+        // the staging array, half a node at a time.
+        constexpr int kLE = kRmax * 32 / kFT;   // elements per thread
+        const int c = tid & 31;
+        T lv[kLE];
+#pragma unroll
+        for (int e = 0; e < kLE; ++e) {
+            const int i = (tid >> 5) + (kFT / 32) * e;
+            lv[e] = (i < nr && c < bk) ? base[(long)sMap[i] * ld + c] : (T)0;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int e = 0; e < kLE / 2; ++e) sStage[(tid >> 5) + (kFT / 32) * e][c] = lv[e + kLE / 2 * h];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kFR / 2; ++k)
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) x[k + kFR / 2 * h][cc] = sStage[lane + 64 * k][4 * w + cc];
+            __syncthreads();
         }
     }
     STAMP(2);
@@ -417,86 +447,87 @@ __device__ __forceinline__ void factor_body(FactorLds<T> &L, const int grp, T *_
     PH_STORE;
     STAMP(4);
 
-    // ---- T (LAPACK larft): T[:, j] = -tau_j T[:, :j] (V^T v_j)[:j], T[j][j] = tau_j
-    // Lane a of wave 0 keeps row a of T in registers (fully unrolled, static
-    // indices); z = V^T V (strict upper part) is read from sZ as broadcasts.
+    // ---- T and the outputs ---------------------------------------------------
+    // Wave 0 forms T (LAPACK larft: T[:, j] = -tau_j T[:, :j] (V^T v_j)[:j],
+    // T[j][j] = tau_j; lane a keeps row a in registers, fully unrolled; z = V^T V
+    // from sZ as broadcasts) and writes it; waves 1..7 meanwhile write V
+    // (kRmax x 32 row-major), VT (32 x kRmax, lanes -> consecutive rows) and R /
+    // zeros back into the matrix for their own columns and, from an LDS copy,
+    // for wave 0's.  R: TR = true along columns from registers (coalesced);
+    // TR = false the 32 x 32 triangle from registers and the zeros below it by
+    // 256-byte rows.
     T *Tm = Tws + (size_t)grp * 32 * 32;
-    if (tid < 32) {
-        const int a = tid;
-        T trow[32];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            T s4[4] = {(T)0, (T)0, (T)0, (T)0};
-#pragma unroll
-            for (int cc = 0; cc < j; ++cc) s4[cc & 3] = fma(trow[cc], sZ[cc][j], s4[cc & 3]);
-            const T s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-            const T tj = j < kk ? sTau[j] : (T)0;
-            trow[j] = a < j ? -tj * s : (a == j ? tj : (T)0);
-        }
-#pragma unroll
-        for (int j = 0; j < 32; ++j) sT[a][j] = trow[j];
-    }
-    STAMP(5);
-    // ---- outputs ------------------------------------------------------------
-    // V (kRmax x 32 row-major) and VT (32 x kRmax, coalesced) from registers;
-    // R / zeros back into the matrix: coalesced from registers for TR = true,
-    // through the staging tile (256-byte rows) for TR = false.
     T *V = Vws + (size_t)grp * kRmax * 32;
     T *VT = VTws + (size_t)grp * 32 * kRmax;
     const int nrp = (nr + 15) & ~15;
-    T iu[4];
+    if (w == 0) {
 #pragma unroll
-    for (int cc = 0; cc < 4; ++cc) iu[cc] = sU1[4 * w + cc];
+        for (int k = 0; k < kFR; ++k)
 #pragma unroll
-    for (int k = 0; k < kFR; ++k) {
-        const int i = lane + 64 * k;
-        T v[4];
+            for (int cc = 0; cc < 4; ++cc) L.sX0[lane + 64 * k][cc] = x[k][cc];
+    }
+    __syncthreads();
+    STAMP(5);
+    if (w == 0) {
+        if (lane < 32) {
+            const int a = lane;
+            T trow[32];
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = 4 * w + cc;
-            v[cc] = (T)0;
-            if (c < kk && i < nr) v[cc] = i < c ? (T)0 : (i == c ? (T)1 : x[k][cc] * iu[cc]);
+            for (int j = 0; j < 32; ++j) {
+                T s4[4] = {(T)0, (T)0, (T)0, (T)0};
+#pragma unroll
+                for (int cc = 0; cc < j; ++cc) s4[cc & 3] = fma(trow[cc], sZ[cc][j], s4[cc & 3]);
+                const T s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                const T tj = j < kk ? sTau[j] : (T)0;
+                trow[j] = a < j ? -tj * s : (a == j ? tj : (T)0);
+            }
+#pragma unroll
+            for (int j = 0; j < 32; ++j) sT[a][j] = trow[j];
         }
-        if (i < nrp) {
+        wave_sync();
+        for (int e = lane; e < 32 * 32; e += 64) Tm[e] = sT[e >> 5][e & 31];
+    } else {
+        // rows lane + 64k of columns c0 .. c0+3 (values xv)
+        auto emit = [&](const T (&xv)[4], int c0, int k) {
+            const int i = lane + 64 * k;
+            T v[4];
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
-                V[(size_t)i * 32 + 4 * w + cc] = v[cc];
-                VT[(size_t)(4 * w + cc) * kRmax + i] = v[cc];   // lanes -> consecutive i
+                const int c = c0 + cc;
+                v[cc] = (T)0;
+                if (c < kk && i < nr) v[cc] = i < c ? (T)0 : (i == c ? (T)1 : xv[cc] * sU1[c]);
             }
-        }
-        if constexpr (TR) {
-            if (i < nr) {
+            if (i < nrp) {
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    V[(size_t)i * 32 + c0 + cc] = v[cc];
+                    VT[(size_t)(c0 + cc) * kRmax + i] = v[cc];
+                }
+            }
+            if (i < nr && (TR || i < 32)) {
                 const int pr = sMap[i];
 #pragma unroll
                 for (int cc = 0; cc < 4; ++cc) {
-                    const int c = 4 * w + cc;
-                    if (c < bk) *vptr<TR>(base, ld, pr, c) = (c >= i) ? x[k][cc] : (T)0;
+                    const int c = c0 + cc;
+                    if (c < bk) *vptr<TR>(base, ld, pr, c) = (c >= i) ? xv[cc] : (T)0;
                 }
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < kFR; ++k) emit(x[k], 4 * w, k);
+        for (int k = w - 1; k < kFR; k += kFT / 64 - 1) {
+            T x0[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) x0[cc] = L.sX0[lane + 64 * k][cc];
+            emit(x0, 0, k);
+        }
+        if constexpr (!TR) {   // zeros below the triangle, rows 32 .. nr-1
+            for (int e = tid - 64; e < (nr - 32) * 32; e += kFT - 64) {
+                const int i = 32 + (e >> 5), c = e & 31;
+                if (c < bk) base[(long)sMap[i] * ld + c] = (T)0;
             }
         }
     }
-    if constexpr (!TR) {
-        const int c = tid & 31;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int k = 0; k < kFR / 2; ++k)
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const int i = lane + 64 * (k + kFR / 2 * h), cg = 4 * w + cc;
-                    sStage[lane + 64 * k][cg] = (cg >= i) ? x[k + kFR / 2 * h][cc] : (T)0;
-                }
-            __syncthreads();
-#pragma unroll
-            for (int e = 0; e < kRmax / 2 / 16; ++e) {
-                const int r = (tid >> 5) + 16 * e, i = kRmax / 2 * h + r;
-                if (i < nr && c < bk) *vptr<false>(base, ld, sMap[i], c) = sStage[r][c];
-            }
-            __syncthreads();
-        }
-    }
-    __syncthreads();
-    for (int e = tid; e < 32 * 32; e += kFT) Tm[e] = sT[e >> 5][e & 31];
     STAMP(6);
 }
 

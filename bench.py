@@ -24,9 +24,9 @@ its own matrices (weak scaling).  The step time is the max over ranks and
 `value` is the whole-job GFLOP/s.
 
 What `value` measures (config.value_kind): the throughput of a STREAM of
-independent reductions -- K matrices (default 20) issued back to back on 4
-lanes of HIP stream pairs (one GPU; matrix j on lane j mod 4, stage 2 of a
-lane's matrix beside stage 1 of its next one; `--pipeline on`, the default),
+independent reductions -- K matrices (default 20) issued back to back on 8
+lanes of HIP stream pairs (matrix j on lane j mod 8, stage 2 of a lane's
+matrix beside stage 1 of its next one; `--pipeline on`, the default),
 fill and drain inside the timed region.  The same K steps one reduction at a
 time on one lane (the reference's per-instance timing, timing.h:79-82) are
 reported as `one_at_a_time`, and `latency_ms_per_reduction` is one matrix's
@@ -88,7 +88,7 @@ def parse():
                    help="pipelined, one GPU: also time K steps without the overlap (reported as one_at_a_time)")
     p.add_argument("--lanes", type=int, default=None,
                    help="pipelined: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
-                        "(default 4; across GPUs each lane has its own RCCL communicator)")
+                        "(default 8; across GPUs each lane has its own RCCL communicator)")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -299,7 +299,7 @@ def maybe_spawn(args) -> None:
 def main():
     args = parse()
     if args.lanes is None:
-        args.lanes = 4 if args.pipeline == "on" else 1
+        args.lanes = 8 if args.pipeline == "on" else 1
     # Every lane launches on two HIP streams; with the runtime's default of 4
     # hardware queues per process, streams beyond that share a queue and
     # their work serialises (measured: 2 lanes 14.1 -> 17.8 TFLOP/s once each
@@ -358,13 +358,17 @@ def main():
     # i, so it runs beside stage 1 of the lane's next matrix (stage 2 is a
     # latency-bound chain on a few dozen CUs, stage 1 HBM-bound on the rest);
     # otherwise s_b's work is ordered after all of s_a's and vice versa (one
-    # reduction at a time).  L lanes side by side (default 4), matrix j on lane
+    # reduction at a time).  L lanes side by side (default 8), matrix j on lane
     # j mod L (the library keeps a workspace -- and, across GPUs, an RCCL
     # communicator -- per launch stream), so one lane's latency-bound work
     # (leaf factors, tail panels, the stage-2 chase, the distributed panel
     # loop's collectives) overlaps another lane's HBM-bound trailing updates.
     # Measured at N = 8192 fp64 (20 steps, one hardware queue per stream):
-    # L = 1 14.1 TFLOP/s, L = 2 18.2, L = 4 19.9, L = 8 20.3.
+    # L = 1 14.1 TFLOP/s, L = 2 18.2, L = 4 19.9, L = 8 20.3; again this round
+    # 4 vs 8: 19.78 vs 20.13 on one GPU and, through the distributed path at
+    # world size 1 over RCCL (--force-dist, 12 steps), 14.6 vs 16.0 -- across
+    # GPUs a matrix's stage 1 is a chain of per-panel collectives and factors,
+    # so more matrices in flight hide more of it.
     lanes = args.lanes if pipelined else 1
     sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
     sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]

@@ -363,10 +363,11 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
         hipLaunchKernelGGL((k_get_R<T>), dim3(1), dim3(32, 32), 0, s, Rloc, Q, (long)lda, bk, nrow);
         D_TRY(C.allgather(Rloc, Rall, (size_t)bk * bk * sz, s));
         const int first = (k + 1) % P;   // the stack starts with the owner of panel k+1
-        for (int q = 0; q < P; ++q) {
-            const int pos = (q - first + P) % P;
-            D_HIP(hipMemcpyAsync(Stk + (size_t)pos * bk * bk, Rall + (size_t)q * bk * bk, (size_t)bk * bk * sz,
-                                 hipMemcpyDeviceToDevice, s));
+        {   // rank q's block to position (q - first) mod P: a rotation, two copies
+            const size_t bb = (size_t)bk * bk;
+            D_HIP(hipMemcpyAsync(Stk, Rall + first * bb, (P - first) * bb * sz, hipMemcpyDeviceToDevice, s));
+            if (first > 0)
+                D_HIP(hipMemcpyAsync(Stk + (P - first) * bb, Rall, first * bb * sz, hipMemcpyDeviceToDevice, s));
         }
         const Tree tr = make_tree(P * bk, bk);
         tree_ws_carve(tr, sz, wsroot, wsr);

@@ -754,12 +754,26 @@ __device__ __forceinline__ int prog_min(const int *p) {
     for (int w = 1; w < W; ++w) m = min(m, lds_acq(p + w));
     return m;
 }
-constexpr int kWriteRows = 32;  // rows per writer batch (at most)
-constexpr int kSubRows = 8;     // rows per writer sub-chunk (registers)
-constexpr int kFly = 48;        // loader: rows in flight (LDS-DMA), <= 63
-constexpr int kChunk = 8;       // loader: rows published per wait
+// (BRD_S2_* macros: developer A/B builds, tools/variant_lib.sh; measured at
+// N = 8192 fp64, round 2: 63 rows in flight 87.3 vs 87.6 ms, 4-row loader
+// chunks 93.2, 16-row writer batches 89.0, compute waves at s_setprio 2 87.2 --
+// and two or three LDS-DMA loader waves dealing the rows in chunks 89.4 /
+// 91.5: the loader's rate is not what holds the chain)
+#ifndef BRD_S2_WRITE_ROWS
+#define BRD_S2_WRITE_ROWS 32
+#endif
+#ifndef BRD_S2_FLY
+#define BRD_S2_FLY 48
+#endif
+#ifndef BRD_S2_CHUNK
+#define BRD_S2_CHUNK 8
+#endif
+constexpr int kWriteRows = BRD_S2_WRITE_ROWS;  // rows per writer batch (at most)
+constexpr int kSubRows = 8;                    // rows per writer sub-chunk (registers)
+constexpr int kFly = BRD_S2_FLY;               // loader: rows in flight (LDS-DMA), <= 63
+constexpr int kChunk = BRD_S2_CHUNK;           // loader: rows published per wait
 
-// s_waitcnt vmcnt(k) for a run-time k in [0, 48] (the immediate must be a constant)
+// s_waitcnt vmcnt(k) for a run-time k in [0, 63] (the immediate must be a constant)
 __device__ __forceinline__ void wait_vmcnt(int k) {
     switch (k) {
 #define BRD_VMCNT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
@@ -773,6 +787,9 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
         BRD_VMCNT_CASE(36) BRD_VMCNT_CASE(37) BRD_VMCNT_CASE(38) BRD_VMCNT_CASE(39) BRD_VMCNT_CASE(40)
         BRD_VMCNT_CASE(41) BRD_VMCNT_CASE(42) BRD_VMCNT_CASE(43) BRD_VMCNT_CASE(44) BRD_VMCNT_CASE(45)
         BRD_VMCNT_CASE(46) BRD_VMCNT_CASE(47) BRD_VMCNT_CASE(48)
+        BRD_VMCNT_CASE(49) BRD_VMCNT_CASE(50) BRD_VMCNT_CASE(51) BRD_VMCNT_CASE(52) BRD_VMCNT_CASE(53)
+        BRD_VMCNT_CASE(54) BRD_VMCNT_CASE(55) BRD_VMCNT_CASE(56) BRD_VMCNT_CASE(57) BRD_VMCNT_CASE(58)
+        BRD_VMCNT_CASE(59) BRD_VMCNT_CASE(60) BRD_VMCNT_CASE(61) BRD_VMCNT_CASE(62) BRD_VMCNT_CASE(63)
 #undef BRD_VMCNT_CASE
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
@@ -862,6 +879,9 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
             // previous sweep to finish task t + 3.
             const int sw = wave / W, pw = wave - sw * W;
             const int i = i0 + sw;
+#ifdef BRD_S2_PRIO
+            __builtin_amdgcn_s_setprio(BRD_S2_PRIO);
+#endif
             SweepIter it;
             it.init(n, n, b, i, sigma);
             const int prev_ntask = sw > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
@@ -932,6 +952,9 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     if (wave == 0 && t == 0) S2STAMP(beta, 1);
                 }
             }
+#ifdef BRD_S2_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             if (lane == 0 && wave == 0) S2STAMP(beta, 2);
             if (lane == 0 && wave == W * nsw - 1) S2STAMP(beta, 3);
         } else if (wave == W * S) {

@@ -240,6 +240,22 @@ int api_apply_target() {
     return ov > 0 ? std::max(32, device_cus() - ov) : 256;
 }
 
+// Least slabs per apply workgroup at tree level `level`.  Beside other work
+// (brd_set_overlap: a stream of reductions, CU time is what counts) an
+// upper-level apply -- one node of stacked R rows, latency-bound, one slab
+// per workgroup when the trailing matrix is narrow -- takes at least 8 slabs
+// per workgroup so that each workgroup's V-fragment load is spread over more
+// than one slab: N = 8192 fp64 stream 20.7-21.0 -> 21.4 TFLOP/s (floor 4:
+// 21.4, 16: 21.3; a floor of 3 at level 0: no gain).  One reduction at a
+// time (latency) the grid stays as wide as the target.
+// BRD_S1_MINRUN0 / BRD_S1_MINRUN1 override (levels 0 / >= 1).
+int api_min_run(int level) {
+    static const char *mr0 = getenv("BRD_S1_MINRUN0"), *mr1 = getenv("BRD_S1_MINRUN1");
+    const char *mr = level == 0 ? mr0 : mr1;
+    if (mr) return std::max(1, atoi(mr));
+    return (level > 0 && g_ctx.overlap_cus > 0) ? 8 : 1;
+}
+
 static int s2_waves() {
     if (g_ctx.overlap_cus > 0) return g_ctx.overlap_cus;
     static int nw = 0;

@@ -71,6 +71,7 @@ hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStr
 int api_fail(int code, const char *msg);           // sets brd_last_error, returns code
 hipStream_t api_stream();                          // the library stream
 int api_apply_target();                            // workgroups per stage-1 apply launch
+int api_min_run(int level);                        // least slabs per apply workgroup at a tree level
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
 // Profiling with kernel-bracketing events: a ProfScope in "launch" mode arms a

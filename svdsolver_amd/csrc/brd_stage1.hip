@@ -1018,10 +1018,7 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
     const int tgt = std::max(1, target - nfac);
     int spw = std::max(1, (groups * nslabs + tgt - 1) / tgt);
     while (spw < nslabs && (long)groups * ((nslabs + spw - 1) / spw) > tgt) ++spw;
-    // tuning (A/B): a floor on the run length per level (0 / 1+)
-    static const char *mr0 = getenv("BRD_S1_MINRUN0"), *mr1 = getenv("BRD_S1_MINRUN1");
-    const char *mr = level == 0 ? mr0 : mr1;
-    if (mr && atoi(mr) > 1) spw = std::min(nslabs, std::max(spw, atoi(mr)));
+    spw = std::min(nslabs, std::max(spw, api_min_run(level)));   // (brd_api.cpp)
     const T *V = (const T *)ws.V[level], *VT = (const T *)ws.VT[level], *Tm = (const T *)ws.T[level];
     // Row-major view: the slab can stay in registers (apply_body's direct
     // path).  Measured at N = 8192 (same box): fp32 stage 1 62.7 -> 61.5 ms;

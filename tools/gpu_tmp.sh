@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 A="--steps,16,--warmup,4,--one-at-a-time,off"
-bash tools/bench_ab.sh "base||$A" "m1_4|BRD_S1_MINRUN1=4|$A" "m1_8|BRD_S1_MINRUN1=8|$A" "m0_3|BRD_S1_MINRUN0=3|$A" "m0_3m1_4|BRD_S1_MINRUN0=3 BRD_S1_MINRUN1=4|$A" "m1_16|BRD_S1_MINRUN1=16|$A" "base2||$A"
+bash tools/bench_ab.sh "base||$A" "t112|BRD_S1_TARGET=112|$A" "t160|BRD_S1_TARGET=160|$A" "t192|BRD_S1_TARGET=192|$A" "t128|BRD_S1_TARGET=128|$A" "base2||$A" "r0|BRD_S2_RAMP=0|$A"

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -494,8 +495,23 @@ int brd_dist_init(int rank, int nranks, const void *id, int id_bytes) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
     auto c = std::make_unique<brd::RcclComm>();
-    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
-    if (r != ncclSuccess) return brd::rccl_fail(r, "ncclCommInitRank");
+    // Several communicators run at once (one per launch stream: several
+    // matrices in flight), each collective a kernel that waits for its peers
+    // on the other GPUs.  Capped at a few blocks per collective, the kernels
+    // of all communicators fit on the CUs together, so no GPU can fill up
+    // with collectives whose peers are still queued behind it (the
+    // multi-communicator hang); the per-panel messages are <= b x m elements,
+    // latency-bound, so the cap costs little bandwidth.  BRD_RCCL_MAX_CTAS
+    // overrides (0 = RCCL's default).
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    static const char *cenv = getenv("BRD_RCCL_MAX_CTAS");
+    const int max_ctas = cenv ? atoi(cenv) : 8;
+    if (max_ctas > 0) {
+        cfg.minCTAs = 1;
+        cfg.maxCTAs = max_ctas;
+    }
+    ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
+    if (r != ncclSuccess) return brd::rccl_fail(r, "ncclCommInitRankConfig");
     c->rank = rank;
     c->nranks = nranks;
     brd::g_comms.add(brd::api_stream(), std::move(c));

@@ -270,16 +270,6 @@ static int s2_waves() {
     return nw;
 }
 
-// Worker ramp of the stage-2 bundle grid (percent of the grid per remaining
-// fraction of the matrix, k_band2bd_bundle): beside stage 1 (brd_set_overlap)
-// idle sweep workgroups hand their CUs back as the chain nears the end; alone
-// the grid stays whole.  BRD_S2_RAMP overrides (0 = off).
-static int s2_ramp() {
-    static const char *renv = getenv("BRD_S2_RAMP");
-    if (renv) return std::max(0, atoi(renv));
-    return g_ctx.overlap_cus > 0 ? 125 : 0;
-}
-
 static hipEvent_t get_event() {
     if (!g_ctx.event_pool.empty()) {
         hipEvent_t e = g_ctx.event_pool.back();
@@ -368,7 +358,7 @@ static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sigma, 
     if (rc) return rc;
     {
         ProfScope ps("s2_sweep", 0, 0, s);
-        HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, sigma, prog, err, s2_waves(), s, s2_ramp()));
+        HIP_TRY(launch_band2bd<T>(A, n, lda, b, exact, sigma, prog, err, s2_waves(), s));
     }
     if (sync) {
         int code = 0;

@@ -62,7 +62,7 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
 // Stage-2 launchers (brd_stage2.hip).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,
-                          int nwaves, hipStream_t s, int ramp = 0);
+                          int nwaves, hipStream_t s);
 template <typename T>
 hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStream_t s);
 

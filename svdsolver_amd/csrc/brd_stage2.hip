@@ -726,7 +726,6 @@ struct BundleFlags {
     int freed;       // ring slots of rows < freed may be reused (writer wave)
     int avail;       // rows < avail have been written back by bundle beta-1 (poller wave)
     int xr[16];      // wave pairs: the task (+1) whose reflector source this wave has read
-    int beta;        // the bundle this workgroup works on (-1: none left for it)
 };
 
 __device__ __forceinline__ int lds_acq(const int *p) {
@@ -841,8 +840,7 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
 
 template <typename T, bool EXACT, int KB, int W>
 __global__ void __launch_bounds__((bundle_max_threads<T, W>()))
-k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err,
-                 int ramp)
+k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int P = ring_pitch<T>(b);
@@ -855,30 +853,7 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
     const RingAcc<T> acc{ring, P, R, b - 1, magic};
     const int nbundles = (n - 1 + S - 1) / S;
 
-    // Bundles are taken in order from a counter (rows_done[n], zeroed with the
-    // flags): bundle beta waits only on bundle beta-1, which a running
-    // workgroup has already taken, so the chain never waits on a workgroup
-    // that is not resident.  With ramp > 0 (stage 2 beside stage-1 work on
-    // other streams) workgroup w stops taking bundles once fewer than w are
-    // needed: the bundles in flight at once scale with a bundle's lifetime,
-    // i.e. with the rows left below it (n - S beta), so the grid shrinks
-    // linearly to 2 workgroups and the CUs go back to stage 1.
-    int *ticket = rows_done + n;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            int bt = -1;
-            const int peek = ld_c(ticket);
-            const long left = (long)n - (long)S * peek;
-            const int need = ramp > 0 ? 2 + (int)((long)gridDim.x * ramp * left / (100L * n)) : (int)gridDim.x;
-            if (peek < nbundles && (int)blockIdx.x < need) {
-                bt = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (bt >= nbundles) bt = -1;
-            }
-            F->beta = bt;
-        }
-        __syncthreads();
-        const int beta = F->beta;
-        if (beta < 0) break;
+    for (int beta = blockIdx.x; beta < nbundles; beta += gridDim.x) {
         const int i0 = beta * S;
         const int nsw = min(S, n - 1 - i0);
         if (threadIdx.x < 16) {
@@ -1265,7 +1240,7 @@ static int coresident_limit(const void *fn, int threads, size_t lds) {
 // reset here: a nonzero value from an earlier launch stays visible).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,
-                          int nwaves, hipStream_t s, int ramp)
+                          int nwaves, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(prog, 0, sizeof(int) * (size_t)(n + 1), s);
     if (e != hipSuccess) return e;
@@ -1295,15 +1270,15 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err, ramp);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 4)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err, ramp);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (W == 2)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err, ramp);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else if (fast32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err, ramp);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err, ramp);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const void *pfn = exact_order ? (const void *)k_band2bd_pipe<T, true> : (const void *)k_band2bd_pipe<T, false>;
@@ -1324,8 +1299,8 @@ hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStr
     return hipGetLastError();
 }
 
-template hipError_t launch_band2bd<double>(double *, int, long, int, bool, bool, int *, int *, int, hipStream_t, int);
-template hipError_t launch_band2bd<float>(float *, int, long, int, bool, bool, int *, int *, int, hipStream_t, int);
+template hipError_t launch_band2bd<double>(double *, int, long, int, bool, bool, int *, int *, int, hipStream_t);
+template hipError_t launch_band2bd<float>(float *, int, long, int, bool, bool, int *, int *, int, hipStream_t);
 template hipError_t launch_extract_bidiag<double>(const double *, int, long, double *, double *, hipStream_t);
 template hipError_t launch_extract_bidiag<float>(const float *, int, long, float *, float *, hipStream_t);
 

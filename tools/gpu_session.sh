@@ -54,11 +54,13 @@ for st in "$@"; do
         env $v timeout -k 5 200 python tools/s1time.py ${n:-8192} "$v" ${dt:-f64} 2>&1 | tail -1 || exit 1
       done ;;
     s2)
-      n=${arg%%:*}; vars=${arg#*:}; [ "$vars" = "$arg" ] && vars="BASE=1"
+      # s2[:N[:VARS[:DT]]]
+      n=$(echo "$arg" | cut -d: -f1); vars=$(echo "$arg" | cut -s -d: -f2); dt=$(echo "$arg" | cut -s -d: -f3)
+      [ -z "$vars" ] && vars="BASE=1"
       rm -f /tmp/s2time_ref.npy
       IFS=';' read -ra VS <<< "$vars"
       for v in "${VS[@]}"; do
-        env $v timeout -k 5 200 python tools/s2time.py ${n:-8192} "$v" 2>&1 | tail -1 || exit 1
+        env $v timeout -k 5 200 python tools/s2time.py ${n:-8192} "$v" ${dt:-f64} 2>&1 | tail -1 || exit 1
       done ;;
     py)
       f=${arg%%:*}; a=${arg#*:}; [ "$a" = "$arg" ] && a=""

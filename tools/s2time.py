@@ -13,9 +13,10 @@ import svdsolver_amd as S  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 tag = sys.argv[2] if len(sys.argv) > 2 else "run"
+dt = torch.float32 if (len(sys.argv) > 3 and sys.argv[3] == "f32") else torch.float64
 b = 32
 g = torch.Generator(device="cuda").manual_seed(5)
-A0 = torch.rand(n, n, dtype=torch.float64, device="cuda", generator=g) * 4 + 1
+A0 = torch.rand(n, n, dtype=dt, device="cuda", generator=g) * 4 + 1
 i = torch.arange(n, device="cuda")
 mask = (i[None, :] >= i[:, None]) & (i[None, :] - i[:, None] <= b)
 A0 = A0 * mask
@@ -35,4 +36,4 @@ if not os.path.exists(ref):
 else:
     r = np.load(ref)
     dev = float(np.linalg.norm(np.abs(dd) - np.abs(r)) / np.linalg.norm(r))
-print(f"{tag}: stage2 n={n} median {np.median(ts):.2f} ms (runs {', '.join(f'{t:.1f}' for t in ts)}) |d| dev vs first {dev:.2e}")
+print(f"{tag}: stage2 n={n} {dt} median {np.median(ts):.2f} ms (runs {', '.join(f'{t:.1f}' for t in ts)}) |d| dev vs first {dev:.2e}")

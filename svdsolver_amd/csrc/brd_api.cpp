@@ -249,6 +249,8 @@ int api_apply_target() {
 // 21.4, 16: 21.3; a floor of 3 at level 0: no gain).  One reduction at a
 // time (latency) the grid stays as wide as the target.
 // BRD_S1_MINRUN0 / BRD_S1_MINRUN1 override (levels 0 / >= 1).
+bool api_overlap_active() { return g_ctx.overlap_cus > 0; }
+
 int api_min_run(int level) {
     static const char *mr0 = getenv("BRD_S1_MINRUN0"), *mr1 = getenv("BRD_S1_MINRUN1");
     const char *mr = level == 0 ? mr0 : mr1;

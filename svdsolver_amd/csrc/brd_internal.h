@@ -72,6 +72,7 @@ int api_fail(int code, const char *msg);           // sets brd_last_error, retur
 hipStream_t api_stream();                          // the library stream
 int api_apply_target();                            // workgroups per stage-1 apply launch
 int api_min_run(int level);                        // least slabs per apply workgroup at a tree level
+bool api_overlap_active();                         // brd_set_overlap reservation in force
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
 // Profiling with kernel-bracketing events: a ProfScope in "launch" mode arms a

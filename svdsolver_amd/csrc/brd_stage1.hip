@@ -925,8 +925,11 @@ __device__ __forceinline__ void apply_body(ApplyLds<T> &L, const int grp, const 
     }   // LDS-staged path
 }
 
-template <typename T, bool TR, bool DIRECT>
-__global__ void __launch_bounds__(kAT)
+// OCC = apply workgroups per CU the kernel is compiled for (the launch
+// bound's second argument is waves per SIMD: 2 OCC).  OCC = 2 (fp32, LDS-staged
+// slab, <= 128 VGPRs) is the stream-of-reductions variant, see launch_apply.
+template <typename T, bool TR, bool DIRECT, int OCC = 1>
+__global__ void __launch_bounds__(kAT, 2 * OCC)
 k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
         const T *__restrict__ VTws, const T *__restrict__ Tws)
 {
@@ -942,8 +945,8 @@ k_apply(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *_
 // the side stream and its two event hand-offs per panel side (about 6-7 us of
 // idle GPU each, measured).  Row y = 0 is dispatched first, so the factor
 // starts at once on a CU of its own.
-template <typename T, bool TR, bool DIRECT>
-__global__ void __launch_bounds__(kAT)
+template <typename T, bool TR, bool DIRECT, int OCC = 1>
+__global__ void __launch_bounds__(kAT, 2 * OCC)
 k_apply_factor(T *__restrict__ base, long ld, LvArgs la, int ncols, int spw, const T *__restrict__ Vws,
                const T *__restrict__ VTws, const T *__restrict__ Tws, T *__restrict__ fbase, long fld, LvArgs fa,
                int nfac, T *__restrict__ fV, T *__restrict__ fVT, T *__restrict__ fT)
@@ -1026,14 +1029,29 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
     // 2-waves-per-SIMD kernel and spills), so fp64 keeps the LDS-staged path.
     // BRD_S1_DIRECT=0 / 1 overrides (tuning).
     static const char *denv = getenv("BRD_S1_DIRECT");
-    const bool want = denv ? denv[0] == '1' : sizeof(T) == 4;
+    // fp32 beside other work (brd_set_overlap): the LDS-staged slab compiled
+    // for two workgroups per CU (<= 128 VGPRs; another lane's workgroup hides
+    // this one's per-slab phases).  N = 8192 fp32 stream, same box, 20 steps,
+    // three pairs: 28.8-28.9 -> 29.8-30.2 TFLOP/s; one reduction at a time it
+    // was slower (stage 1 60.7 -> 62.9 ms), so alone the one-per-CU variants
+    // stay.  BRD_S1_OCC2 = 0 / 1 overrides.
+    static const char *oenv = getenv("BRD_S1_OCC2");
+    const bool occ2 = sizeof(T) == 4 && (oenv ? oenv[0] == '1' : api_overlap_active());
+    const bool want = denv ? denv[0] == '1' : (sizeof(T) == 4 && !occ2);
     const int direct = !trans && want && (level == 0 || t.bk % 16 == 0) &&
                                ((long)t.M * ld + ncols) * (long)sizeof(T) < (1L << 31) ? 1 : 0;
     if (fuse) {
         dim3 grid(groups, 1 + (nslabs + spw - 1) / spw), block(kAT);
         const LvArgs fa = lv_args(t, level + 1);
         T *fV = (T *)ws.V[level + 1], *fVT = (T *)ws.VT[level + 1], *fT = (T *)ws.T[level + 1];
-        if (trans)
+        if (occ2 && !direct) {
+            if (trans)
+                launch_timed((k_apply_factor<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
+                             fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+            else
+                launch_timed((k_apply_factor<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
+                             fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+        } else if (trans)
             launch_timed((k_apply_factor<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         else if (direct)
@@ -1045,7 +1063,10 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
         return hipGetLastError();
     }
     dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
-    if (trans)
+    if (occ2 && !direct) {
+        if (trans) launch_timed((k_apply<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
+        else       launch_timed((k_apply<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
+    } else if (trans)
         launch_timed((k_apply<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
     else if (direct)
         launch_timed((k_apply<T, false, true>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);

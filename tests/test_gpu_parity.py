@@ -363,6 +363,39 @@ def test_reduce_many_pipelined_matches_serial(S, lanes):
         assert np.all(B[~inb] == 0)
 
 
+def test_stage1_f32_overlap_matches_serial(S):
+    """fp32 stage 1 under a brd_set_overlap reservation runs the trailing update
+    compiled for two workgroups per CU (LDS-staged slab, launch_apply's occ2),
+    alone the register-resident variant: both issue the same MFMA chain on the
+    same operands, so the band is bit for bit the serial one (including the
+    upper-level applies' 8-slab floor, which only regroups slabs)."""
+    import torch
+    rng = np.random.default_rng(47)
+    n, b, k = 1024, 32, 3
+    As = [rng.uniform(0, 5, (n, n)).astype(np.float32) for _ in range(k)]
+    ref = []
+    for A in As:
+        dA = torch.from_numpy(A).cuda()
+        S.ge2band(dA, b)
+        ref.append(dA.cpu().numpy())
+    mats = [torch.from_numpy(A).cuda() for A in As]
+    s_a = torch.cuda.Stream()
+    S.set_overlap(S.overlap_cus(n))
+    try:
+        with torch.cuda.stream(s_a):
+            for M in mats:
+                S.ge2band(M, b, sync=False)
+        torch.cuda.synchronize()
+    finally:
+        S.set_overlap(0)
+    i, j = np.indices((n, n))
+    inb = (j >= i) & (j - i <= b)
+    for M, R in zip(mats, ref):
+        B = M.cpu().numpy()
+        assert np.array_equal(B, R)
+        assert np.all(B[~inb] == 0)
+
+
 def test_padded_leading_dimension(S):
     """Row-strided device matrices (lda = n + pad, the C ABI's lda): the band
     and the sigma bidiagonal's singular values match the contiguous run, and

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -39,3 +41,33 @@ def test_torchrun_command_passes_size_through():
     ns = get_args_parser().parse_args(cmd[3:])
     assert ns.nproc_per_node == "2" and ns.training_script.endswith("bench.py")
     assert ns.training_script_args == ["--gpus", "2", "--size", "4096", "--steps", "3", "--warmup", "1"]
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_end_to_end():
+    """The driver's N > 1 bench path, end to end on one GPU: two ranks under
+    torch.distributed.run, stage 1 sharded over them, bands gathered on rank
+    j mod 2, stage 2 beside the next matrices, the lanes' communicators --
+    through the host-callback communicator (RCCL needs one GPU per rank).
+    Rank 0 prints one JSON line with n_gpus = 2 and a positive value."""
+    import json
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--comm", "host", "--size", "1024", "--steps", "3", "--warmup", "1",
+           "--lanes", "2", "--cpu-baseline", "off"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["n"] == 1024
+    assert d["config"]["matrices_per_timed_region"] == 3

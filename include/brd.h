@@ -74,6 +74,14 @@ int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigne
 int brd_bdsvd_f64(const double *d, const double *e, int n, double *sv);
 int brd_bdsvd_f32(const float *d, const float *e, int n, float *sv);
 
+/* The same on the GPU: d (n), e (n-1) and sv (n) are DEVICE pointers; the
+ * values (descending) are bracketed by multisection on the Golub-Kahan
+ * tridiagonal (every value independently, G lanes each), to the host QR's
+ * accuracy (|sigma_i - exact| ~ eps sigma_max).  Runs on the library stream;
+ * BRD_ASYNC returns without waiting.  e may be NULL when n = 1. */
+int brd_bdsvd_dev_f64(const double *d, const double *e, int n, double *sv, unsigned flags);
+int brd_bdsvd_dev_f32(const float *d, const float *e, int n, float *sv, unsigned flags);
+
 /* Stream used by subsequent calls (hipStream_t; NULL = the legacy default
  * stream).  Until the first call the library uses a stream of its own;
  * brd_use_own_stream() reverts to it. */

@@ -40,7 +40,7 @@ EXPORTED = (
     "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_check_errors", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
     "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
-    "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_last_error", "brd_version",
+    "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_bdsvd_dev_f64", "brd_bdsvd_dev_f32", "brd_last_error", "brd_version",
 )
 
 # brd_coll_fn (include/brd.h): int (*)(int op, const void *send, void *recv,
@@ -83,6 +83,9 @@ def _load() -> ctypes.CDLL:
         h = getattr(L, f"brd_bdsvd_{t}")
         h.argtypes = [vp, vp, ci, vp]
         h.restype = ci
+        hd = getattr(L, f"brd_bdsvd_dev_{t}")
+        hd.argtypes = [vp, vp, ci, vp, cu]
+        hd.restype = ci
     L.brd_set_stream.argtypes = [vp]
     L.brd_set_stream.restype = ci
     L.brd_use_own_stream.argtypes = []
@@ -255,6 +258,38 @@ def bdsvd(d, e):
     _check(fn, getattr(lib, fn)(ctypes.c_void_p(d.ctypes.data), ctypes.c_void_p(ep.ctypes.data), n,
                                 ctypes.c_void_p(sv.ctypes.data)))
     return sv
+
+
+def bdsvd_gpu(d, e, *, sync: bool = True):
+    """Singular values (descending) of the upper bidiagonal (d, e) on the GPU:
+    multisection on the Golub-Kahan tridiagonal, every value bracketed on its
+    own (brd_bdsvd_dev_*; the host twin is :func:`bdsvd`).  d, e: torch CUDA
+    tensors of one dtype (e has n - 1 entries); returns a CUDA tensor."""
+    import torch
+    if not (_is_torch_cuda(d) and (_is_torch_cuda(e) or d.shape[0] == 1)):
+        raise ValueError("bdsvd_gpu takes torch CUDA tensors (use bdsvd for host arrays)")
+    d = d.contiguous()
+    n = d.shape[0]
+    if e.shape[0] != max(n - 1, 0):
+        raise ValueError("e must have n - 1 entries")
+    e = e.to(d.dtype).contiguous()
+    sfx = _sfx(d.dtype)
+    sv = torch.empty_like(d)
+    _bind_stream(d)
+    fn = f"brd_bdsvd_dev_{sfx}"
+    _check(fn, getattr(lib, fn)(ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(e.data_ptr() if n > 1 else 0), n,
+                                ctypes.c_void_p(sv.data_ptr()), 0 if sync else BRD_ASYNC))
+    return sv
+
+
+def singular_values_gpu(A, b: int = 32):
+    """Singular values of the square torch CUDA matrix A, every step on the GPU:
+    stage 1, stage 2 with the sigma-preserving geometry, :func:`bdsvd_gpu`.
+    A is not modified; returns a CUDA tensor (descending)."""
+    M = A.clone()
+    ge2band(M, b)
+    d, e = band2bd(M, b, sigma=True)
+    return bdsvd_gpu(d, e)
 
 
 def singular_values(A, b: int = 32):

@@ -563,6 +563,25 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
     return BRD_OK;
 }
 
+// Bidiagonal singular values on the GPU (device pointers; brd_bdsvd_dev.hip).
+// The workspace (2n + 1 elements: the squared Golub-Kahan off-diagonals, the
+// scale and the bound) is the launch stream's cached staging buffer.
+template <typename T>
+static int bdsvd_dev(const T *d, const T *e, int n, T *sv, unsigned flags) {
+    std::lock_guard<std::mutex> lk(g_ctx.mu);
+    if (n < 1) return fail(BRD_EINVAL, "need n >= 1 (n=%d)", n);
+    if (!d || !sv || (n > 1 && !e)) return fail(BRD_EINVAL, "d, e (n > 1) and sv must be device pointers");
+    if (!is_device_ptr(d) || !is_device_ptr(sv) || (n > 1 && !is_device_ptr(e)))
+        return fail(BRD_EINVAL, "brd_bdsvd_dev: d, e and sv must be device memory");
+    void *ws = nullptr;
+    int rc = ensure_stage(sizeof(T) * (2 * (size_t)n + 1), &ws);
+    if (rc) return rc;
+    hipStream_t s = stream();
+    HIP_TRY(launch_bdsvd_dev<T>(d, n > 1 ? e : d, n, sv, (T *)ws, s));
+    if (!(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
+    return BRD_OK;
+}
+
 }  // namespace brd
 
 // ==========================================================================
@@ -581,6 +600,13 @@ int brd_band2bd_f64(double *A, int n, int lda, int b, double *d, double *e, unsi
 }
 int brd_band2bd_f32(float *A, int n, int lda, int b, float *d, float *e, unsigned flags) {
     return brd::band2bd<float>(A, n, lda, b, d, e, flags);
+}
+
+int brd_bdsvd_dev_f64(const double *d, const double *e, int n, double *sv, unsigned flags) {
+    return brd::bdsvd_dev<double>(d, e, n, sv, flags);
+}
+int brd_bdsvd_dev_f32(const float *d, const float *e, int n, float *sv, unsigned flags) {
+    return brd::bdsvd_dev<float>(d, e, n, sv, flags);
 }
 
 int brd_set_stream(void *hip_stream) {

@@ -66,6 +66,10 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
 template <typename T>
 hipError_t launch_extract_bidiag(const T *A, int n, long lda, T *d, T *e, hipStream_t s);
 
+// Bidiagonal singular values on the GPU (brd_bdsvd_dev.hip); ws >= 2n + 1 elements.
+template <typename T>
+hipError_t launch_bdsvd_dev(const T *d, const T *e, int n, T *sv, T *ws, hipStream_t s);
+
 // ---- services of the C-ABI layer (brd_api.cpp) used by the distributed
 // driver (brd_dist.hip) ------------------------------------------------------
 int api_fail(int code, const char *msg);           // sets brd_last_error, returns code

@@ -1044,14 +1044,18 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
         dim3 grid(groups, 1 + (nslabs + spw - 1) / spw), block(kAT);
         const LvArgs fa = lv_args(t, level + 1);
         T *fV = (T *)ws.V[level + 1], *fVT = (T *)ws.VT[level + 1], *fT = (T *)ws.T[level + 1];
-        if (occ2 && !direct) {
-            if (trans)
-                launch_timed((k_apply_factor<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
-                             fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
-            else
-                launch_timed((k_apply_factor<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
-                             fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
-        } else if (trans)
+        if constexpr (sizeof(T) == 4) {   // (the two-per-CU build exists for fp32 only)
+            if (occ2 && !direct) {
+                if (trans)
+                    launch_timed((k_apply_factor<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT,
+                                 Tm, fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+                else
+                    launch_timed((k_apply_factor<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT,
+                                 Tm, fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
+                return hipGetLastError();
+            }
+        }
+        if (trans)
             launch_timed((k_apply_factor<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm,
                                fuse_panel, fuse_ld > 0 ? fuse_ld : ld, fa, nfac, fV, fVT, fT);
         else if (direct)
@@ -1063,10 +1067,14 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level, 
         return hipGetLastError();
     }
     dim3 grid(groups, (nslabs + spw - 1) / spw), block(kAT);
-    if (occ2 && !direct) {
-        if (trans) launch_timed((k_apply<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
-        else       launch_timed((k_apply<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
-    } else if (trans)
+    if constexpr (sizeof(T) == 4) {
+        if (occ2 && !direct) {
+            if (trans) launch_timed((k_apply<T, true, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
+            else       launch_timed((k_apply<T, false, false, 2>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
+            return hipGetLastError();
+        }
+    }
+    if (trans)
         launch_timed((k_apply<T, true, false>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);
     else if (direct)
         launch_timed((k_apply<T, false, true>), grid, block, s, base, ld, a, ncols, spw, V, VT, Tm);

@@ -15,7 +15,7 @@
 // One group of G lanes per singular value: each lane evaluates the count at
 // one of G interior points of the value's interval [lo, hi], a ballot over the
 // group picks the sub-interval that holds the value (log2(G + 1) bits per
-// round, ~17 rounds for fp64 with G = 8), and every lane of the group
+// round, ~13 rounds for fp64 with G = 16), and every lane of the group
 // recomputes the points itself, so the group never exchanges data beyond the
 // ballot.  All lanes of a wave walk the same squared off-diagonals a^2 in the
 // same order (broadcast loads).  The matrix is scaled by its largest entry so
@@ -31,7 +31,17 @@
 
 namespace brd {
 
-constexpr int kBdG = 8;         // lanes per singular value
+// Lanes per singular value (n = 8192 fp64, same box: 4 lanes 22.9 ms, 8 17.0,
+// 16 15.6; the count loop unrolled by 4: 16 lanes 13.5 ms, 8 13.9; the IEEE
+// division instead of the refined reciprocal: 26.5 at 8 lanes).
+#ifndef BRD_BD_LANES
+#define BRD_BD_LANES 16
+#endif
+#ifndef BRD_BD_UNROLL
+#define BRD_BD_UNROLL 4
+#endif
+constexpr int kBdG = BRD_BD_LANES;
+static_assert(kBdG >= 2 && kBdG <= 16 && (kBdG & (kBdG - 1)) == 0, "2..16 lanes, a power of two");
 constexpr int kBdBlock = 256;   // threads per workgroup (32 values)
 
 template <typename T> struct BdEps;
@@ -84,14 +94,33 @@ __global__ void __launch_bounds__(1024) k_bd_prep(const T *__restrict__ d, const
     }
 }
 
+// 1/q: the hardware reciprocal refined by Newton steps to full precision
+// (fewer instructions than the IEEE division sequence; the count only needs
+// the sign of each pivot, which the refined quotient keeps).
+__device__ __forceinline__ double bd_rcp(double q) {
+    double r = __builtin_amdgcn_rcp(q);
+    r = fma(r, fma(-q, r, 1.0), r);
+    r = fma(r, fma(-q, r, 1.0), r);
+    return r;
+}
+__device__ __forceinline__ float bd_rcp(float q) {
+    const float r = __builtin_amdgcn_rcpf(q);
+    return fmaf(r, fmaf(-q, r, 1.0f), r);
+}
+
 // #{sigma < x} for x > 0: negative pivots of T_GK - x I, less n.
 template <typename T>
 __device__ __forceinline__ int bd_count(const T *__restrict__ a2, int m, T x, T pivmin) {
     T q = -x;
     int neg = 1;   // q_1 = -x < 0
+#pragma unroll BRD_BD_UNROLL
     for (int i = 0; i < m; ++i) {
         if (fabs(q) < pivmin) q = -pivmin;
+#ifdef BRD_BD_IEEE_DIV
         q = -x - a2[i] / q;
+#else
+        q = fma(-a2[i], bd_rcp(q), -x);
+#endif
         neg += q < (T)0 ? 1 : 0;
     }
     return neg - (m + 1) / 2;

@@ -17,11 +17,12 @@
 //       separated, no trailing newline) for its plotting notebook.  Stage 2 is
 //       timed too: printed on the same line and written in the same 2-line
 //       format to <csv stem>_stage2.csv.
-//   svd_gpu svd <N> [--dtype f32|f64] [--band B]
+//   svd_gpu svd <N> [--dtype f32|f64] [--band B] [--host-values]
 //       Singular values of an N x N matrix uniform in [0,5): stage 1, stage 2 with
-//       the sigma-preserving geometry (BRD_SIGMA) and the host bidiagonal QR
-//       (brd_bdsvd_*, the reference's serial::qrd step); prints the largest and
-//       smallest values and the time of each step (not in the reference CLI).
+//       the sigma-preserving geometry (BRD_SIGMA) and the bidiagonal's values
+//       on the GPU (brd_bdsvd_dev_*; --host-values: the host QR brd_bdsvd_*, the
+//       reference's serial::qrd step); prints the largest and smallest values
+//       and the time of each step (not in the reference CLI).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -31,6 +32,8 @@
 #include <fstream>
 #include <string>
 #include <vector>
+
+#include <hip/hip_runtime.h>
 
 #include "brd.h"
 #include "brd_matrix.hpp"
@@ -53,6 +56,28 @@ template <> int band2bd_sigma<float>(float *A, int n, int b, float *d, float *e)
 template <typename T> int bdsvd(const T *d, const T *e, int n, T *sv);
 template <> int bdsvd<double>(const double *d, const double *e, int n, double *sv) { return brd_bdsvd_f64(d, e, n, sv); }
 template <> int bdsvd<float>(const float *d, const float *e, int n, float *sv) { return brd_bdsvd_f32(d, e, n, sv); }
+template <typename T> int bdsvd_dev(const T *d, const T *e, int n, T *sv);
+template <> int bdsvd_dev<double>(const double *d, const double *e, int n, double *sv) {
+    return brd_bdsvd_dev_f64(d, e, n, sv, 0);
+}
+template <> int bdsvd_dev<float>(const float *d, const float *e, int n, float *sv) {
+    return brd_bdsvd_dev_f32(d, e, n, sv, 0);
+}
+// The bidiagonal's values on the GPU from host d, e: copies in, brd_bdsvd_dev_*, copy out.
+template <typename T>
+int bdsvd_gpu(const T *d, const T *e, int n, T *sv) {
+    T *g = nullptr;
+    if (hipMalloc(&g, sizeof(T) * (3 * (size_t)n)) != hipSuccess) return BRD_ENOMEM;
+    T *gd = g, *ge = g + n, *gs = g + 2 * (size_t)n;
+    int rc = BRD_OK;
+    if (hipMemcpy(gd, d, sizeof(T) * n, hipMemcpyHostToDevice) != hipSuccess ||
+        (n > 1 && hipMemcpy(ge, e, sizeof(T) * (n - 1), hipMemcpyHostToDevice) != hipSuccess))
+        rc = BRD_EHIP;
+    if (!rc) rc = bdsvd_dev<T>(gd, ge, n, gs);
+    if (!rc && hipMemcpy(sv, gs, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = BRD_EHIP;
+    hipFree(g);
+    return rc;
+}
 
 void die(const char *what, int rc) {
     std::fprintf(stderr, "%s failed (%d): %s\n", what, rc, brd_last_error());
@@ -149,7 +174,7 @@ int benchmark(int step, int nsteps, int ninst, int b, const std::string &csv) {
 }
 
 template <typename T>
-int svd(int n, int b) {
+int svd(int n, int b, bool host_values) {
     brd::Matrix<T> A(n, n);
     A.fill(T(0), T(5), 1000003ull * n);
     std::vector<T> d(n), e(n), sv(n);
@@ -160,12 +185,13 @@ int svd(int n, int b) {
     rc = band2bd_sigma<T>(A.data(), n, b, d.data(), e.data());
     if (rc) die("brd_band2bd (BRD_SIGMA)", rc);
     auto t2 = std::chrono::steady_clock::now();
-    rc = bdsvd<T>(d.data(), e.data(), n, sv.data());
-    if (rc) die("brd_bdsvd", rc);
+    rc = host_values ? bdsvd<T>(d.data(), e.data(), n, sv.data()) : bdsvd_gpu<T>(d.data(), e.data(), n, sv.data());
+    if (rc) die(host_values ? "brd_bdsvd" : "brd_bdsvd_dev", rc);
     auto t3 = std::chrono::steady_clock::now();
     auto sec = [](auto a, auto z) { return std::chrono::duration<double>(z - a).count(); };
     std::printf("N = %d (%s, band %d): dense -> band %g sec | band -> bidiagonal %g sec | bidiagonal -> "
-                "values %g sec (host)\n", n, sizeof(T) == 8 ? "fp64" : "fp32", b, sec(t0, t1), sec(t1, t2), sec(t2, t3));
+                "values %g sec (%s)\n", n, sizeof(T) == 8 ? "fp64" : "fp32", b, sec(t0, t1), sec(t1, t2), sec(t2, t3),
+                host_values ? "host" : "GPU");
     const int k = std::min(n, 5);
     std::printf("largest :");
     for (int i = 0; i < k; ++i) std::printf(" %.12g", (double)sv[i]);
@@ -184,8 +210,9 @@ void help() {
                 "\n(2) Correctness test against the reference fixtures (band size 4).\n"
                 "\t>> check [64|512|1024] [--dtype f32|f64] [--data-dir DIR]\n"
                 "\tExample: ./svd_gpu check 64\n"
-                "\n(3) Singular values (stage 1, sigma-preserving stage 2, host bidiagonal QR).\n"
-                "\t>> svd [<int> N] [--dtype f32|f64] [--band B]\n"
+                "\n(3) Singular values (stage 1, sigma-preserving stage 2, the bidiagonal's values on the GPU;\n"
+                "\t    --host-values: the host bidiagonal QR).\n"
+                "\t>> svd [<int> N] [--dtype f32|f64] [--band B] [--host-values]\n"
                 "\tExample: ./svd_gpu svd 2048 --dtype f64\n");
 }
 
@@ -195,6 +222,7 @@ int main(int argc, char **argv) {
     std::string dtype = "f32", dir = getenv("BRD_DATA_DIR") ? getenv("BRD_DATA_DIR") : "data",
                 csv = "data/cuda_2_benchmark.csv";
     int band = 32;
+    bool host_values = false;
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -202,6 +230,7 @@ int main(int argc, char **argv) {
         else if (a == "--data-dir" && i + 1 < argc) dir = argv[++i];
         else if (a == "--csv" && i + 1 < argc) csv = argv[++i];
         else if (a == "--band" && i + 1 < argc) band = std::atoi(argv[++i]);
+        else if (a == "--host-values") host_values = true;
         else pos.push_back(a);
     }
     if (pos.size() >= 2 && pos[0] == "check") {
@@ -215,7 +244,7 @@ int main(int argc, char **argv) {
     }
     if (pos.size() >= 2 && pos[0] == "svd") {
         const int n = std::atoi(pos[1].c_str());
-        return dtype == "f64" ? svd<double>(n, band) : svd<float>(n, band);
+        return dtype == "f64" ? svd<double>(n, band, host_values) : svd<float>(n, band, host_values);
     }
     help();
     return 0;

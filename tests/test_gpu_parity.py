@@ -311,15 +311,29 @@ def test_one_stage_band1_is_bidiagonal_with_input_singular_values(S, T):
 
 def test_cli_svd_runs(S):
     """svd_gpu svd: the C++ caller of the whole pipeline (stage 1, sigma stage 2,
-    brd_bdsvd) runs and prints descending singular values."""
+    the bidiagonal's values on the GPU, brd_bdsvd_dev) prints descending
+    singular values, the same as with the host QR (--host-values)."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(S.LIB_PATH), "..", "bin", "svd_gpu")
-    out = subprocess.run([exe, "svd", "512", "--dtype", "f64"], capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0, out.stderr
-    line = [ln for ln in out.stdout.splitlines() if ln.startswith("largest")][0]
-    vals = [float(x) for x in line.split(":")[1].split()]
-    assert len(vals) == 5 and all(a >= b for a, b in zip(vals, vals[1:])) and vals[0] > 0
+
+    def run(*extra):
+        out = subprocess.run([exe, "svd", "512", "--dtype", "f64", *extra], capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr
+        lines = out.stdout.splitlines()
+        big = [float(x) for x in [ln for ln in lines if ln.startswith("largest")][0].split(":")[1].split()]
+        small = [float(x) for x in [ln for ln in lines if ln.startswith("smallest")][0].split(":")[1].split()]
+        return big, small, out.stdout
+
+    big, small, text = run()
+    assert "(GPU)" in text
+    assert len(big) == 5 and all(a >= b for a, b in zip(big, big[1:])) and big[0] > 0
+    hbig, hsmall, htext = run("--host-values")
+    assert "(host)" in htext
+    # the printed values carry 12 significant digits
+    assert np.allclose(big, hbig, rtol=1e-10, atol=1e-10 * big[0])
+    assert np.allclose(small, hsmall, rtol=0, atol=1e-10 * big[0])
 
 
 @pytest.mark.parametrize("lanes", [1, 3])

@@ -258,15 +258,49 @@ struct Reflector {
 };
 // LAPACK-style (tau = 0 when the sub-column is zero) from the squared norm
 // of the sub-column and the diagonal entry x0.
+// (BRD_S1_IEEE_REFL: the IEEE sqrt and divisions instead of the hardware
+// reciprocal square root / reciprocal refined by Newton steps -- the scalars
+// sit on the column loop's critical path, once per column of every panel)
+__device__ __forceinline__ double refl_rsq(double q) {
+    double r = __builtin_amdgcn_rsq(q);
+    const double h = 0.5 * q;
+    r = r * fma(-h * r, r, 1.5);
+    r = r * fma(-h * r, r, 1.5);
+    return r;
+}
+__device__ __forceinline__ float refl_rsq(float q) {
+    const float r = __builtin_amdgcn_rsqf(q);
+    return r * fmaf(-0.5f * q * r, r, 1.5f);
+}
+__device__ __forceinline__ double refl_rcp(double u) {
+    double y = __builtin_amdgcn_rcp(u);
+    y = fma(y, fma(-u, y, 1.0), y);
+    y = fma(y, fma(-u, y, 1.0), y);
+    return y;
+}
+__device__ __forceinline__ float refl_rcp(float u) {
+    const float y = __builtin_amdgcn_rcpf(u);
+    return fmaf(y, fmaf(-u, y, 1.0f), y);
+}
 template <typename T>
 __device__ __forceinline__ Reflector<T> make_reflector(T sub2, T x0) {
     Reflector<T> h{(T)1, (T)0, x0};
     if (sub2 != (T)0) {
+#ifdef BRD_S1_IEEE_REFL
         const T nrm = sqrt(fma(x0, x0, sub2));
         h.alpha = x0 >= (T)0 ? -nrm : nrm;
         const T u1 = x0 - h.alpha;
         h.tau = -u1 / h.alpha;
         h.inv_u1 = (T)1 / u1;
+#else
+        const T s2 = fma(x0, x0, sub2);
+        const T r = refl_rsq(s2);   // 1 / ||x||
+        const T nrm = s2 * r;
+        h.alpha = x0 >= (T)0 ? -nrm : nrm;
+        const T u1 = x0 - h.alpha;
+        h.tau = x0 >= (T)0 ? u1 * r : -u1 * r;   // -u1 / alpha
+        h.inv_u1 = refl_rcp(u1);
+#endif
     }
     return h;
 }

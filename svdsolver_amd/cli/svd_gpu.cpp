@@ -75,7 +75,7 @@ int bdsvd_gpu(const T *d, const T *e, int n, T *sv) {
         rc = BRD_EHIP;
     if (!rc) rc = bdsvd_dev<T>(gd, ge, n, gs);
     if (!rc && hipMemcpy(sv, gs, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = BRD_EHIP;
-    hipFree(g);
+    (void)hipFree(g);
     return rc;
 }
 

@@ -532,11 +532,12 @@ __device__ __forceinline__ void factor_body(FactorLds<T> &L, const int grp, T *_
                 if (c < kk && i < nr) v[cc] = i < c ? (T)0 : (i == c ? (T)1 : xv[cc] * sU1[c]);
             }
             if (i < nrp) {
+                // the lane's four V entries are one aligned 4-wide row segment:
+                // one vector store instead of four scattered scalar ones
+                using T4 = T __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<T4 *>(V + (size_t)i * 32 + c0) = T4{v[0], v[1], v[2], v[3]};
 #pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    V[(size_t)i * 32 + c0 + cc] = v[cc];
-                    VT[(size_t)(c0 + cc) * kRmax + i] = v[cc];
-                }
+                for (int cc = 0; cc < 4; ++cc) VT[(size_t)(c0 + cc) * kRmax + i] = v[cc];
             }
             if (i < nr && (TR || i < 32)) {
                 const int pr = sMap[i];

@@ -35,6 +35,16 @@ static int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// Device error word codes (sticky per launch stream; brd_check_errors).
+static const char *err_word_text(int code) {
+    switch (code) {
+        case 1: return "stage-2 pipeline stalled (spin limit hit)";
+        case 2: return "stage-1 panel cluster barrier timed out";
+        case 3: return "stage-1 CholeskyQR panel breakdown";
+        default: return "device error";
+    }
+}
+
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
         hipError_t e_ = (expr);                                                           \
@@ -367,8 +377,8 @@ static int band2bd_device(T *A, int n, long lda, int b, bool exact, bool sigma, 
         rc = take_s2_error(slot(), &code);
         if (rc) return rc;
         if (code)
-            return fail(BRD_EHIP, "stage-2 pipeline stalled (spin limit hit, code %d) in this or an earlier "
-                                  "asynchronous call on this stream", code);
+            return fail(BRD_EHIP, "%s (code %d) in this or an earlier asynchronous call on this stream",
+                        err_word_text(code), code);
     }
     return BRD_OK;
 }
@@ -415,15 +425,33 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
     return BRD_OK;
 }
 
+// Blocked stage 1 (brd_stage1_blk.hip) for b = 32 -- the delayed two-sided
+// update -- over all but the last panels; BRD_S1_BLOCKED=0 keeps the
+// per-panel path throughout (A/B and parity against the per-panel kernels).
+static bool blocked_enabled() {
+    const char *env = getenv("BRD_S1_BLOCKED");   // read per call: tests switch it between calls
+    return env && env[0] == '1';
+}
+
 template <typename T>
-static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s) {
+static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s, bool *used_blocked = nullptr) {
+    const bool blk_ok = blocked_enabled() && b == 32 && lda % 2 == 0 && ((uintptr_t)A % 16) == 0;
+    const int kend = blk_ok ? blk_columns(n, b) : 0;
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
+    if (kend > 0) need = std::max(need, blk_ws_bytes(m, n, sizeof(T)));
     void *wsbase = nullptr;
     int rc = ensure_ws(need, &wsbase);
     if (rc) return rc;
+    if (used_blocked) *used_blocked = kend > 0;
+    if (kend > 0) {
+        int *prog = nullptr, *err = nullptr;
+        rc = ensure_s2_flags(n, &prog, &err);
+        if (rc) return rc;
+        HIP_TRY(blk_ge2band<T>(A, m, n, lda, wsbase, s, api_apply_target(), err));
+    }
     TreeWs ws;
-    for (int k = 0; k < n; k += b) {
+    for (int k = kend; k < n; k += b) {
         const int bk = std::min(b, n - k);
         const int mp = m - k;
         const int n2 = n - k - bk;
@@ -490,8 +518,9 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
     const bool dev = (flags & BRD_DEVICE_PTR) != 0;
     if (dev && !is_device_ptr(A)) return fail(BRD_EINVAL, "BRD_DEVICE_PTR set but A is not device memory");
     int rc;
+    bool blocked = false;
     if (dev) {
-        rc = ge2band_device<T>(A, m, n, lda, b, s);
+        rc = ge2band_device<T>(A, m, n, lda, b, s, &blocked);
         if (rc == BRD_OK && !(flags & BRD_ASYNC)) HIP_TRY(hipStreamSynchronize(s));
     } else {
         void *stage = nullptr;
@@ -500,7 +529,7 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
         T *d = (T *)stage;
         HIP_TRY(hipMemcpy2DAsync(d, sizeof(T) * n, A, sizeof(T) * lda, sizeof(T) * n, m,
                                  hipMemcpyHostToDevice, s));
-        rc = ge2band_device<T>(d, m, n, n, b, s);
+        rc = ge2band_device<T>(d, m, n, n, b, s, &blocked);
         if (rc == BRD_OK)
             HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, m,
                                      hipMemcpyDeviceToHost, s));
@@ -509,6 +538,12 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
     if (rc == BRD_OK) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(BRD_EHIP, "stage 1: %s", hipGetErrorString(e));
+        if (blocked && (!dev || !(flags & BRD_ASYNC))) {
+            int code = 0;
+            rc = take_s2_error(slot(), &code);
+            if (rc) return rc;
+            if (code) return fail(BRD_EHIP, "stage 1: %s (code %d)", err_word_text(code), code);
+        }
     }
     return rc;
 }
@@ -637,8 +672,8 @@ int brd_check_errors(void) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return brd::fail(BRD_EHIP, "HIP error: %s", hipGetErrorString(e));
     if (!bad.empty())
-        return brd::fail(BRD_EHIP, "stage-2 pipeline stalled in an asynchronous call (spin limit hit, code %s)",
-                         bad.c_str());
+        return brd::fail(BRD_EHIP, "device error word set in an asynchronous call (1: stage-2 spin limit, "
+                                    "2: stage-1 cluster barrier, 3: stage-1 panel breakdown; codes %s)", bad.c_str());
     return BRD_OK;
 }
 

@@ -59,6 +59,16 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
                         int ncols, const TreeWs &ws, hipStream_t s, int target = 256,
                         T *fuse_panel = nullptr, long fuse_ld = 0);
 
+// Blocked stage 1 (brd_stage1_blk.hip): panels of width 32 grouped in blocks
+// of 4 with a delayed two-sided update.  blk_columns: columns [0, kend) the
+// blocked path reduces (0 when it does not apply); the caller finishes the
+// remaining panels with the per-panel path.  err: device error word (2:
+// cluster barrier timeout, 3: CholeskyQR breakdown).
+size_t blk_ws_bytes(int m, int n, size_t elem);
+int blk_columns(int n, int b);
+template <typename T>
+hipError_t blk_ge2band(T *A, int m, int n, long lda, void *ws, hipStream_t s, int target, int *err);
+
 // Stage-2 launchers (brd_stage2.hip).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,

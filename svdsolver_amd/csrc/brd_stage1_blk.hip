@@ -1,0 +1,1564 @@
+// Stage 1, blocked: dense -> band with a delayed two-sided update (gfx950).
+//
+// Replaces, for panels of width 32, the per-panel structure of the
+// reference's cuda_brd_p1 (svd_cuda_2.cu:1117-1220: QR of the column panel,
+// qr_apply_cuda :1039 over the whole trailing matrix, LQ of the row panel,
+// lq_apply_cuda :1081 over it again).  Inside a block of nb panels the
+// trailing matrix is not written; it is kept as
+//
+//     A_cur = A - Lw RwT          Lw  (m x 256) = [V_0..V_3 | X_0..X_3]
+//                                 RwT (256 x n) = [Y_0..Y_3 | U_0..U_3]^T
+//
+// (left reflectors I - V_j T_j V_j^T, right reflectors I - U_j S_j U_j^T,
+// Y_j = A_cur^T V_j T_j, X_j = A_cur U_j S_j) and updated once per block by
+// k_blkupd, a rank-2 nb 32 product on the matrix cores.  Per panel:
+//
+//   k_rpass (Y)  partial sums of A^T V_j over row splits, and G = Lw^T V_j
+//   k_prep (LQ)  Y_j = (A^T V_j - Rw G) T_j, the corrected row panel
+//   k_cqr        QR of the row panel's transpose: CholeskyQR2 + Householder
+//                reconstruction -> U_j, S_j, the band's L block
+//   k_rpass (X)  partial sums of A U_j over column splits, and G = Rw^T U_j
+//   k_prep (QR)  X_j = (A U_j - Lw G) S_j, the next corrected column panel
+//   k_cqr        QR of the column panel -> V_{j+1}, T_{j+1}, the band's R block
+//
+// The executable specification (same steps, same workspaces) is
+// tests/s1_model.py; DESIGN.md "Stage 1, blocked" has the roofline of each
+// kernel.
+#include "brd_internal.h"
+
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+#include <cstdio>
+#include <vector>
+
+namespace brd {
+namespace blk {
+
+// --------------------------------------------------------------------------
+// MFMA 16x16x4, one operand element per lane:
+//   A operand lane l: A[m = l&15][k = l>>4],  B operand lane l: B[k = l>>4][n = l&15]
+//   D register g of lane l: row crow(l>>4, g), column l&15
+// --------------------------------------------------------------------------
+template <typename T> struct Mf;
+template <> struct Mf<double> {
+    typedef double v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(double a, double b, v4 c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int crow(int q, int g) { return q + 4 * g; }
+};
+template <> struct Mf<float> {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(float a, float b, v4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int crow(int q, int g) { return 4 * q + g; }
+};
+
+template <typename T>
+struct G2 {   // two consecutive elements: 16 B (fp64) / 8 B (fp32)
+    typedef T v2 __attribute__((ext_vector_type(2)));
+};
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ==========================================================================
+// k_rpass: D = B^T S (Y pass) or S B (X pass) for a tall "skinny" operand B
+// (K x 32) and a source S, summed over one split of the K range.
+//   Y pass (YP): S(k, m) = src[k*ld + m] (row-major A, k = rows, m = columns),
+//                D[t][m] = sum_k B[k][t] S(k, m); partials stored [split][t][m].
+//   X pass     : S(k, m) = src[m*ld + k] (k = columns, m = rows),
+//                D[m][t] = sum_k S(k, m) B[k][t]; partials stored [split][m][t].
+// B(k, t) = bsrc[k*bld + t] in both.  Every wave streams its own 64 values of
+// m straight from HBM into MFMA operand registers (no LDS, no barriers):
+//   Y: one 16-byte load per lane and 4 rows gives 2 x 16 columns (even / odd
+//      column tiles), 4 rows x 256 contiguous bytes per instruction;
+//   X: one 16-byte load per lane gives 2 k of one row: 16 rows x 64 bytes per
+//      instruction, two K steps each;
+// with kSU steps of loads in flight (static register ring).  The "virtual"
+// workgroups (the first ksplit of the grid) compute the same product with
+// S = vsrc (256 wide); they meet at a counter and each sums one slice of
+// their partials into vout in fixed order (deterministic).
+// ==========================================================================
+constexpr int NBMAX = 4;    // panels per block (Lw / RwT hold 2 NBMAX 32 = 256 vectors)
+constexpr int kRT = 256;    // threads (4 waves)
+constexpr int kWM = 64;     // m per wave
+constexpr int kMT = 256;    // m per workgroup
+constexpr int kSU = 8;      // K steps in flight (Y); X: kSU / 2 step pairs
+
+struct RpArgs {
+    const void *src;  long ld;      // source S
+    const void *vsrc; long vld;     // virtual tile source (256 wide), or null
+    const void *bsrc; long bld;     // skinny operand B (k, t) = bsrc[k*bld + t]
+    int K, M;                       // S extents
+    int mtiles, ksplit, kper;       // kper: k per split (multiple of 8)
+    int nvirt;                      // ksplit if there is a virtual tile, else 0
+    void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
+    void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
+    void *vout;                     // virtual result [32][256] / [256][32]
+    int *counter;                   // [0]: virtual-tile barrier, [1]: exit (0 between launches)
+    int *err;
+};
+
+template <typename T, bool YP>
+__global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
+    typedef typename G2<T>::v2 v2;
+    typedef typename Mf<T>::v4 v4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l15 = lane & 15;
+    const int bid = blockIdx.x;
+    const bool virt = bid < a.nvirt;
+    int mx, ks;
+    if (virt) { mx = 0; ks = bid; }
+    else      { const int r = bid - a.nvirt; mx = r % a.mtiles; ks = r / a.mtiles; }
+    const T *S;
+    long ld;
+    int M;
+    if (virt) { S = (const T *)a.vsrc; ld = a.vld; M = kMT; }
+    else      { S = (const T *)a.src + (YP ? (long)mx * kMT : (long)mx * kMT * a.ld); ld = a.ld; M = min(kMT, a.M - mx * kMT); }
+    const T *B = (const T *)a.bsrc;
+    const int kbeg = ks * a.kper, kend = min(a.K, kbeg + a.kper);
+    const int mb = kWM * w;
+    v4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = v4{0, 0, 0, 0};
+
+    if constexpr (YP) {
+        // acc[h*4 + p*2 + e]: t-half h, column pair group p (32 columns), parity e
+        const int nst = kend > kbeg ? (kend - kbeg + 3) / 4 : 0;
+        v2 ra[kSU][2];
+        T rb[kSU][2];
+        auto load = [&](int s, v2 (&va)[2], T (&vb)[2]) {
+            const int k = kbeg + 4 * s + q;
+            const bool kv = k < kend;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int m = mb + 32 * p + 2 * l15;
+                v2 v = {(T)0, (T)0};
+                if (kv && m < M) {
+                    const T *src = S + (long)k * ld + m;
+                    if (m + 1 < M) v = *(const v2 *)src; else v.x = src[0];
+                }
+                va[p] = v;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) vb[h] = kv ? B[(long)k * a.bld + 16 * h + l15] : (T)0;
+        };
+#pragma unroll
+        for (int u = 0; u < kSU; ++u)
+            if (u < nst) load(u, ra[u], rb[u]);
+        for (int s0 = 0; s0 < nst; s0 += kSU) {
+#pragma unroll
+            for (int u = 0; u < kSU; ++u) {
+                const int s = s0 + u;
+                if (s < nst) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int p = 0; p < 2; ++p) {
+                            acc[h * 4 + p * 2 + 0] = Mf<T>::mma(rb[u][h], ra[u][p].x, acc[h * 4 + p * 2 + 0]);
+                            acc[h * 4 + p * 2 + 1] = Mf<T>::mma(rb[u][h], ra[u][p].y, acc[h * 4 + p * 2 + 1]);
+                        }
+                    if (s + kSU < nst) load(s + kSU, ra[u], rb[u]);
+                }
+            }
+        }
+    } else {
+        // acc[p*2 + h]: row tile p (16 rows), t-half h; one step pair = 8 k
+        const int npr = kend > kbeg ? (kend - kbeg + 7) / 8 : 0;
+        constexpr int kSP2 = kSU / 2;
+        v2 ra[kSP2][4];
+        T rb[kSP2][2][2];
+        auto load = [&](int s2, v2 (&va)[4], T (&vb)[2][2]) {
+            const int k = kbeg + 8 * s2 + 2 * q;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int m = mb + 16 * p + l15;
+                v2 v = {(T)0, (T)0};
+                if (m < M && k < kend) {
+                    const T *src = S + (long)m * ld + k;
+                    if (k + 1 < kend) v = *(const v2 *)src; else v.x = src[0];
+                }
+                va[p] = v;
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) vb[e][h] = (k + e < kend) ? B[(long)(k + e) * a.bld + 16 * h + l15] : (T)0;
+        };
+#pragma unroll
+        for (int u = 0; u < kSP2; ++u)
+            if (u < npr) load(u, ra[u], rb[u]);
+        for (int s0 = 0; s0 < npr; s0 += kSP2) {
+#pragma unroll
+            for (int u = 0; u < kSP2; ++u) {
+                const int s2 = s0 + u;
+                if (s2 < npr) {
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            acc[p * 2 + h] = Mf<T>::mma(ra[u][p].x, rb[u][0][h], acc[p * 2 + h]);
+                            acc[p * 2 + h] = Mf<T>::mma(ra[u][p].y, rb[u][1][h], acc[p * 2 + h]);
+                        }
+                    if (s2 + kSP2 < npr) load(s2 + kSP2, ra[u], rb[u]);
+                }
+            }
+        }
+    }
+
+    // ---- partials ----------------------------------------------------------
+    T *out;
+    long mp;
+    if (virt) { out = (T *)a.vpart + (size_t)ks * 32 * kMT; mp = kMT; }
+    else      { out = (T *)a.part + (size_t)ks * 32 * a.mp + (size_t)mx * kMT * (YP ? 1 : 32); mp = a.mp; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = Mf<T>::crow(q, g);
+            if (YP) {
+                const int h = i >> 2, p = (i >> 1) & 1, e = i & 1;
+                const int t = 16 * h + r, m = mb + 32 * p + 2 * l15 + e;
+                if (m < M) out[(size_t)t * mp + m] = acc[i][g];
+            } else {
+                const int p = i >> 1, h = i & 1;
+                const int m = mb + 16 * p + r, t = 16 * h + l15;
+                if (m < M) out[(size_t)m * 32 + t] = acc[i][g];
+            }
+        }
+    if (!virt) return;
+
+    // ---- virtual tile: meet, then each workgroup sums one slice ---------------
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        long spins = 0;
+        while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.nvirt) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1L << 26)) { __hip_atomic_store(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const T *vp = (const T *)a.vpart;
+    const int per = (32 * kMT + a.nvirt - 1) / a.nvirt;
+    const int e0 = ks * per, e1 = min(32 * kMT, e0 + per);
+    for (int e = e0 + tid; e < e1; e += kRT) {
+        T v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v[k] = k < a.nvirt ? vp[(size_t)k * 32 * kMT + e] : (T)0;
+        T s = v[0];
+#pragma unroll
+        for (int k = 1; k < 32; ++k)
+            if (k < a.nvirt) s += v[k];
+        ((T *)a.vout)[e] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(a.counter + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == a.nvirt - 1) {
+            __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.counter + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ==========================================================================
+// k_prep: the per-column (LQ side) / per-row (QR side) corrections, on the
+// matrix cores.  64 items per workgroup, 16 per wave.
+//   LQ (item i = column c+32+i of panel j, c = panel column):
+//     y   = sum_ks part[ks][:][i] - sum_{k in K1} RwT[k][col] G[k][:]     K1 = V_<j, X_<j
+//     Y_j = y T_j                -> RwT[32j + t][col]
+//     q   = A[c+t][col] - sum_{k in K2} Lw[c+t][k] RwT[k][col]           K2 = V_<=j, X_<j
+//                                -> QpT[t][i]
+//     (computed transposed, D[t][i]: the B operand RwT[k][col0 + l15] is one
+//     coalesced load per lane and step, shared by both corrections)
+//   QR (item i = row c+i, c = column of panel j >= 1):
+//     x   = sum_ks part[ks][i][:] - sum_{k in K1} Lw[row][k] G[k][:]      K1 = V_<=j-1, X_<j-1
+//     X_{j-1} = x S_{j-1}        -> Lw[row][128 + 32(j-1) + t]
+//     factor: p = A[row][c+t] - sum_{k in K2} Lw[row][k] RwT[k][c+t]     K2 = V_<j, X_<j -> Qp[i][t]
+//     (D[i][t]: the A operand Lw[row][.] is read as 16-byte pairs, two k
+//     steps each, shared by both corrections)
+// K sets are kept compact in LDS: [0, 32a) and [128, 128 + 32b) stored
+// back to back.
+// ==========================================================================
+constexpr int kPT = 256;
+constexpr int kPI = 64;    // items per workgroup
+
+struct PrepArgs {
+    void *A; long lda;
+    void *Lw; void *RwT; long ldr;
+    const void *part; long mp; int ksplit;
+    const void *G;            // virtual result of the read pass (LQ: [32][256], QR: [256][32])
+    const void *Tm;           // T_j (LQ) / S_{j-1} (QR), 32 x 32 row-major
+    void *Qp;                 // LQ: QpT [32][mq]; QR: Qp [rows][32]
+    long mq;
+    int c;                    // panel column
+    int j;                    // panel index in the block
+    int items;
+    int reduce, factor;       // QR side switches
+};
+
+constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
+constexpr int kLW = 226;
+constexpr int kQP = 40;    // QR pitch (rows k, k + 2 in opposite bank halves)
+
+template <typename T>
+__global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
+    typedef typename Mf<T>::v4 v4;
+    __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
+    __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
+    __shared__ T Tt[32 * 34];    // T_j^T
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l15 = lane & 15;
+    const int j = a.j, c = a.c;
+    const int nk1 = 64 * j, nk2 = 64 * j + 32;
+    const T *G = (const T *)a.G;
+    const T *Lw = (const T *)a.Lw;
+    T *RwT = (T *)a.RwT;
+    // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
+    // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
+    // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
+    if (tid < nk1) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
+    }
+    if (tid < nk2) {
+        const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
+    }
+    {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + kPT * u;
+            Tt[(e & 31) * 34 + (e >> 5)] = v[u];
+        }
+    }
+    __syncthreads();
+
+    const int i0 = blockIdx.x * kPI + 16 * w;
+    const int il = i0 + l15;                       // this lane's item (B operand / C column)
+    const bool iv = il < a.items;
+    const long col = (long)c + 32 + il;
+    const T *A = (const T *)a.A;
+    v4 ay[2], aq[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            ay[h][g] = (T)0;
+            aq[h][g] = iv ? A[(size_t)(c + t) * a.lda + col] : (T)0;
+        }
+    // ---- K1: both corrections share the B operand RwT[k][col] ----------------
+    // all B operands are loaded before the first MFMA (unconditional loads at
+    // clamped addresses, zeroed when out of range): one memory latency, not one per step
+    constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
+    const long colc = iv ? col : (long)c + 32;
+    T b1[kMS], b2[kMS];
+#pragma unroll
+    for (int s = 0; s < kMS; ++s) {
+        const int k1 = min(4 * s + q, max(32 * j - 1, 0)), k2 = 128 + k1;
+        const T v1 = RwT[(size_t)k1 * a.ldr + colc], v2 = RwT[(size_t)k2 * a.ldr + colc];
+        const bool ok = iv && s < 8 * j;
+        b1[s] = ok ? v1 : (T)0;
+        b2[s] = ok ? v2 : (T)0;
+    }
+#pragma unroll
+    for (int s = 0; s < kMS; ++s) {
+        if (s < 8 * j) {
+            const int kk1 = 4 * s + q, kk2 = 32 * j + 4 * s + q;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + kk1], b1[s], ay[h]);
+                aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + kk1], b1[s], aq[h]);                 // V_<j
+                ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + kk2], b2[s], ay[h]);
+                aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + kk2 + 32], b2[s], aq[h]);            // X_<j
+            }
+        }
+    }
+    // ---- y = sum of split partials - correction ------------------------------
+    const T *part = (const T *)a.part;
+    T y[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) y[h][g] = (T)0;
+    const size_t ilc = iv ? il : 0;
+    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
+        T v[4][2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int t = 16 * h + Mf<T>::crow(q, g);
+                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * 32 + t) * a.mp + ilc];
+                }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if (k0 + u < a.ksplit) y[h][g] += v[u][h][g];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) y[h][g] = iv ? y[h][g] - ay[h][g] : (T)0;
+    // ---- Y_j^T = T_j^T y^T: the C registers of y are the B operand -----------
+    v4 ayj[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int u = 16 * hp + Mf<T>::crow(q, g);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) ayj[h] = Mf<T>::mma(Tt[(16 * h + l15) * 34 + u], y[hp][g], ayj[h]);
+        }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            if (iv) RwT[(size_t)(32 * j + t) * a.ldr + col] = ayj[h][g];
+        }
+    // ---- q += -Lw[c+t][32j + u] Y_j[u] ----------------------------------------
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int u = 16 * hp + Mf<T>::crow(q, g);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + 32 * j + u], ayj[hp][g], aq[h]);
+        }
+    T *QpT = (T *)a.Qp;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            if (iv) QpT[(size_t)t * a.mq + il] = aq[h][g];
+        }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
+    typedef typename Mf<T>::v4 v4;
+    typedef typename G2<T>::v2 v2;
+    __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
+    __shared__ T Ss[32 * 48];        // S_{j-1}
+    __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l15 = lane & 15;
+    const int j = a.j, jp = j - 1, c = a.c;
+    const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
+    const int n2 = a.factor ? 64 * j : 0;      // K2 compact: [0, 32j) | [128, 128 + 32j)
+    T *Rs = Gs + n1 * kQP;
+    const T *G = (const T *)a.G;
+    const T *RwT = (const T *)a.RwT;
+    T *Lw = (T *)a.Lw;
+    // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
+    if (tid < n1) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)k * 32 + t];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Gs[kk * kQP + t] = v[t];
+    }
+    if (tid < n2) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + c + t];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Rs[kk * kQP + t] = -v[t];
+    }
+    {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + kPT * u;
+            Ss[(e >> 5) * 48 + (e & 31)] = v[u];
+        }
+    }
+    __syncthreads();
+
+    const int i0 = blockIdx.x * kPI + 16 * w;
+    const int ia = i0 + l15;                        // A-operand row of this lane
+    const bool va = ia < a.items;
+    const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
+    const T *A = (const T *)a.A;
+    v4 ax[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}}, ap[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ic = i0 + Mf<T>::crow(q, g);
+            ap[h][g] = (a.factor && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
+        }
+    // ranges of Lw columns: [0, 32j) (compact 0) and [128, 128 + 32jp)
+    // (compact 32j); lane q takes k = 8s + 2q + e.  All A operands (16-byte
+    // pairs of the lane's row) are loaded before the first MFMA.
+    constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
+    v2 av1[kMP], av2[kMP];
+#pragma unroll
+    for (int s = 0; s < kMP; ++s) {
+        const int kl1 = min(8 * s, max(32 * j - 8, 0)) + 2 * q, kl2 = min(8 * s, max(32 * jp - 8, 0)) + 2 * q;
+        const v2 u1 = *(const v2 *)(lrow + kl1), u2 = *(const v2 *)(lrow + 128 + kl2);
+        av1[s] = (va && s < 4 * j) ? u1 : v2{(T)0, (T)0};
+        av2[s] = (va && s < 4 * jp) ? u2 : v2{(T)0, (T)0};
+    }
+    auto krange = [&](const v2 (&av)[kMP], int cb, int ngrp) {
+#pragma unroll
+        for (int s = 0; s < kMP; ++s) {
+            if (s < ngrp) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int kk = cb + 8 * s + 2 * q + e;
+                    const T x = e ? av[s].y : av[s].x;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        ax[h] = Mf<T>::mma(x, Gs[kk * kQP + 16 * h + l15], ax[h]);
+                        if (a.factor) ap[h] = Mf<T>::mma(x, Rs[kk * kQP + 16 * h + l15], ap[h]);
+                    }
+                }
+            }
+        }
+    };
+    krange(av1, 0, 4 * j);              // V_<j      (K1 and K2)
+    krange(av2, 32 * j, 4 * jp);        // X_<j-1    (K1 and K2)
+    // ---- x = sum of split partials - correction; X_{j-1} = x S ---------------
+    const T *part = (const T *)a.part;
+    T xs[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xs[h][g] = (T)0;
+    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
+        T v[4][2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int ic = min(i0 + Mf<T>::crow(q, g), a.items - 1), t = 16 * h + l15;
+                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * a.mp + ic) * 32 + t];
+                }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if (k0 + u < a.ksplit) xs[h][g] += v[u][h][g];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = Mf<T>::crow(q, g), t = 16 * h + l15;
+            Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] : (T)0;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    v4 xx[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int u = 4 * s + q;
+        const T av = Tb[w][l15 * 34 + u];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) xx[h] = Mf<T>::mma(av, Ss[u * 48 + 16 * h + l15], xx[h]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = Mf<T>::crow(q, g), ic = i0 + r, t = 16 * h + l15;
+            if (ic < a.items) Lw[(size_t)(c + ic) * 256 + 128 + 32 * jp + t] = xx[h][g];
+            Tb[w][r * 34 + t] = xx[h][g];
+        }
+    if (!a.factor) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- p += -X_{j-1}[row][u] RwT[128 + 32jp + u][c+t] -----------------------
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int u = 4 * s + q;
+        const T av = Tb[w][l15 * 34 + u];
+        const int kk = 32 * j + 32 * jp + u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ap[h] = Mf<T>::mma(av, Rs[kk * kQP + 16 * h + l15], ap[h]);
+    }
+    T *Qp = (T *)a.Qp;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ic = i0 + Mf<T>::crow(q, g);
+            if (ic < a.items) Qp[(size_t)ic * 32 + 16 * h + l15] = ap[h][g];
+        }
+}
+
+// ==========================================================================
+// k_cqr: QR of a tall M x 32 panel as a Householder block reflector, by a
+// cluster of workgroups (one thread per row, up to kRPT rows per thread):
+//   Gram G1 = P^T P (power-of-two prescaled per workgroup, summed in fixed
+//   order after a cluster barrier), Cholesky R1, Q1 = P R1^-1, Gram G2
+//   (workgroup 0 also publishes Q1's top 32 rows), second barrier; then
+//   every workgroup, redundantly: Cholesky R2, the top block Q_t = Q1_t R2^-1,
+//   its modified LU Q_t - S = L U (s_j = -sign of the pivot: Ballard et al.
+//   2015), M = U R2, and V = Q1 M^-1 for its rows (rows < 32: L).  Workgroup
+//   0 also forms T = -U S L^-T and R = S R2 R1 and writes them.  Two cluster
+//   barriers per panel; all arithmetic in fp64.
+// A Cholesky pivot that is not positive or below 1e-7 x the largest (panel
+// condition number beyond ~1e7, where CholeskyQR2 loses orthogonality) sets
+// the error word (3).
+// ==========================================================================
+constexpr int kCT = 256;
+constexpr int kRPT = 1;
+constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
+
+struct CqrArgs {
+    const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
+    int M;
+    void *vdst; long vsi, vst;        // V(i, t)
+    void *vdst2; long vsi2, vst2;     // optional second copy of V (null: none)
+    void *tout;                       // T (32 x 32)
+    void *apan; long asi, ast;        // the panel in A: (i, t)
+    int rpt;                          // rows per thread
+    double *ws;                       // cluster scratch (cqr_ws_doubles)
+    int *ctr;                         // [0]: barrier, [1]: exit
+    int *err;
+    unsigned long long *stamps;       // diagnostics (BRD_S1_STAMPS): workgroup 0's phase clocks, or null
+};
+
+// scratch (doubles): the two Gram passes' partials (separate: a fast
+// workgroup writes its second partial while others still sum the first),
+// per-workgroup exponents, Q1's top block
+__host__ __device__ constexpr size_t cqr_ws_doubles(int nwg) { return (size_t)2 * 1024 * 64 + (size_t)nwg + 2048 + 64; }
+
+__device__ __forceinline__ bool cluster_barrier(int *ctr, int target, int *err) {
+    // every workgroup: all threads' stores drained, then one arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int s_ok;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ok = 1;
+        long spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1L << 26)) { ok = 0; __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+struct CqrLds {
+    // the 32 x 32 matrices first: their LDS addresses fit the 16-bit offset field
+    double g[32][kSP];       // reduced Gram
+    double r1[32][kSP];      // R1 (upper, row-major)
+    double r2[32][kSP];      // R2
+    double u[32][kSP];       // LU of the top block: U (upper) and L (strict lower)
+    double mm[32][kSP];      // M = U R2 with the reciprocal diagonal (trsm_row's form)
+    double tq[32][kSP];      // Q1's / Q's top block
+    double r1w[32][kSP];     // R1, R2 in trsm_row's form
+    double r2w[32][kSP];
+    double sgn[32];
+    double emax;
+    int e_w;
+    int flags;
+    double q[4][64][33];     // per-wave staging of 64 rows (Gram); then per-wave Gram partials
+};
+
+__device__ __forceinline__ double rdl(double v, int l) {   // lane l's value, wave-uniform
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// Gram partial of this wave's rows (one per lane) accumulated into gacc
+// (the three distinct 16 x 16 blocks of the symmetric 32 x 32)
+__device__ __forceinline__ void gram_wave(CqrLds &L, int w, int lane, const double (&x)[32], double (&gacc)[3][4]) {
+    typedef Mf<double>::v4 v4;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) L.q[w][lane][t] = x[t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int qq = lane >> 4, l15 = lane & 15;
+    v4 a00 = {gacc[0][0], gacc[0][1], gacc[0][2], gacc[0][3]};
+    v4 a01 = {gacc[1][0], gacc[1][1], gacc[1][2], gacc[1][3]};
+    v4 a11 = {gacc[2][0], gacc[2][1], gacc[2][2], gacc[2][3]};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int k = 4 * s + qq;
+        const double v0 = L.q[w][k][l15], v1 = L.q[w][k][16 + l15];
+        a00 = Mf<double>::mma(v0, v0, a00);
+        a01 = Mf<double>::mma(v0, v1, a01);
+        a11 = Mf<double>::mma(v1, v1, a11);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) { gacc[0][g] = a00[g]; gacc[1][g] = a01[g]; gacc[2][g] = a11[g]; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Cholesky G = R^T R (R upper) by one wave, lane c holding column c in
+// registers, row j of R broadcast by readlanes; R and 1/diag into LDS.
+// False on a non-positive or tiny pivot.
+__device__ __forceinline__ bool chol_wave(const double (&G)[32][kSP], double (&R)[32][kSP], double (&Rw)[32][kSP], int lane) {
+    // lane c: column c in registers; row j of R goes through LDS (R itself)
+    // and comes back as 16-byte broadcast reads: no readlane per element
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const int c = lane & 31;
+    double col[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) col[i] = G[i][c];
+    bool ok = true;
+    double dmax = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const double piv = rdl(col[j], j);
+        const bool good = piv > 0 && piv < 1e300;
+        // 1/sqrt by the hardware estimate and two Newton steps (the division and
+        // IEEE square root sit on the 32-step chain)
+        const double pv = good ? piv : 1.0;
+        double invd = __builtin_amdgcn_rsq(pv);
+        invd = invd * fma(-0.5 * pv * invd, invd, 1.5);
+        invd = invd * fma(-0.5 * pv * invd, invd, 1.5);
+        const double d = pv * invd;
+        dmax = fmax(dmax, d);
+        if (!good || d < 1e-7 * dmax) ok = false;
+        const double r = col[j] * invd;   // R[j][c] (meaningful for c >= j)
+        if (lane < 32) {
+            R[j][c] = c >= j ? r : 0.0;
+            Rw[j][c] = c > j ? r : (c == j ? invd : 0.0);
+        }
+        if (j == 31) break;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        d2 rr[16];
+#pragma unroll
+        for (int p = (j + 1) / 2; p < 16; ++p) rr[p] = *(const d2 *)&R[j][2 * p];
+#pragma unroll
+        for (int i = j + 1; i < 32; ++i) col[i] = fma(-((i & 1) ? rr[i >> 1].y : rr[i >> 1].x), r, col[i]);
+    }
+    return ok;
+}
+
+// x <- x R^-1, right-looking.  Rw: R (upper) with the reciprocal of its
+// diagonal in place of the diagonal, in LDS.  Row k + 1 of Rw is read (as
+// 16-byte pairs, a wave-uniform address: one LDS broadcast per pair) while
+// step k computes, so the reads' latency is hidden behind the FMAs.
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void trsm_row(double (&x)[32], const double (&Rw)[32][kSP]) {
+    d2v cur[16], nxt[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) cur[p] = *(const d2v *)&Rw[0][2 * p];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        if (k + 1 < 32) {
+#pragma unroll
+            for (int p = (k + 1) / 2; p < 16; ++p) nxt[p] = *(const d2v *)&Rw[k + 1][2 * p];
+        }
+        x[k] *= (k & 1) ? cur[k >> 1].y : cur[k >> 1].x;
+        const double xk = x[k];
+#pragma unroll
+        for (int i = k + 1; i < 32; ++i) x[i] = fma(-xk, (i & 1) ? cur[i >> 1].y : cur[i >> 1].x, x[i]);
+        if (k + 1 < 32) {
+#pragma unroll
+            for (int p = (k + 1) / 2; p < 16; ++p) cur[p] = nxt[p];
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // the next row's LDS reads first
+        __builtin_amdgcn_sched_group_barrier(0x2, 64, 0);     // then this step's VALU
+    }
+}
+
+// fixed-order sum of the cluster's Gram partials into L.g: 4 entries per
+// thread, all (<= kCW) partials of an entry loaded at once
+constexpr int kCW = 64;   // most workgroups per cluster (M <= kCW kCT rows)
+// Two-level fixed-order sum of the cluster's Gram partials: workgroup wg
+// sums its slice of the 1024 entries over all partials into gfin, a cluster
+// barrier, then every workgroup reads gfin (8 KB) into L.g.
+__device__ __forceinline__ void gram_reduce(CqrLds &L, const double *gp, const int *ewl, int nwg, int e, bool scaled,
+                                            double *gfin, int wg, int *ctr, int target, int *err) {
+    // gp: [1024][kCW] (entry-major: one entry's partials are contiguous)
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const int tid = threadIdx.x;
+    const int per = (1024 + nwg - 1) / nwg;
+    for (int el = wg * per + tid; el < min(1024, (wg + 1) * per); el += kCT) {
+        d2 v[kCW / 2];
+#pragma unroll
+        for (int k = 0; k < kCW / 2; ++k) v[k] = *(const d2 *)(gp + (size_t)el * kCW + 2 * k);
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < kCW; ++k) {
+            double t = (k & 1) ? v[k >> 1].y : v[k >> 1].x;
+            if (scaled) {
+                const int ek = ewl[k];
+                t = ek != INT_MIN ? ldexp(t, 2 * (ek - e)) : 0.0;
+            }
+            s += k < nwg ? t : 0.0;
+        }
+        gfin[el] = s;
+    }
+    cluster_barrier(ctr, target, err);
+    for (int el = tid; el < 1024; el += kCT) L.g[el >> 5][el & 31] = gfin[el];
+}
+
+#define CQR_STAMP(k)                                                                      \
+    do {                                                                                  \
+        if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr(CqrArgs a) {
+    __shared__ CqrLds L;
+    CQR_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nwg = gridDim.x, wg = blockIdx.x;
+    const int rpt = a.rpt;
+    double *gp1 = a.ws;                               // [1024][kCW] Gram partials, entry-major
+    double *gp2 = a.ws + (size_t)1024 * kCW;          // [1024][kCW]
+    double *ew = a.ws + (size_t)2048 * kCW;           // [nwg] exponents (as doubles)
+    double *q1top = ew + nwg;                         // [32][32]
+    double *gfin = q1top + 1024;                      // [32][32] the reduced Gram
+    const T *src = (const T *)a.src;
+    T *ap = (T *)a.apan;
+    T *vd = (T *)a.vdst;
+    T *vd2 = (T *)a.vdst2;
+
+    // ---- rows into registers ------------------------------------------------
+    double x[kRPT][32];
+    int rowid[kRPT];
+    double amax = 0;
+#pragma unroll
+    for (int r = 0; r < kRPT; ++r) {
+        const int i = (wg * rpt + r) * kCT + tid;
+        rowid[r] = (r < rpt && i < a.M) ? i : -1;
+        const T *srow = src + (size_t)(rowid[r] >= 0 ? i : 0) * a.si;
+        if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
+            typedef typename G2<T>::v2 v2;
+#pragma unroll
+            for (int t = 0; t < 32; t += 2) {
+                const v2 v = *(const v2 *)(srow + t);
+                x[r][t] = (double)v.x;
+                x[r][t + 1] = (double)v.y;
+            }
+        } else {
+            const long st = a.st;
+#pragma unroll
+            for (int t = 0; t < 32; ++t) x[r][t] = (double)srow[t * st];
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            if (rowid[r] < 0) x[r][t] = 0.0;
+            amax = fmax(amax, fabs(x[r][t]));
+        }
+    }
+    // workgroup max -> power-of-two exponent (frexp: amax = f 2^e, 0.5 <= f < 1)
+    {
+        double m = amax;
+        for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        if (tid == 0) L.e_w = INT_MIN;
+        __syncthreads();
+        if (lane == 0) {
+            int e = INT_MIN;
+            if (m > 0) frexp(m, &e);
+            atomicMax(&L.e_w, e);
+        }
+        __syncthreads();
+    }
+    const int e_w = L.e_w;
+    CQR_STAMP(1);
+    if (e_w != INT_MIN) {
+#pragma unroll
+        for (int r = 0; r < kRPT; ++r)
+#pragma unroll
+            for (int t = 0; t < 32; ++t) x[r][t] = ldexp(x[r][t], -e_w);
+    }
+
+    // Gram partial of the rows in registers -> dst (1024 doubles)
+    auto gram_partial = [&](double *dst) {
+        double gacc[3][4] = {};
+#pragma unroll
+        for (int r = 0; r < kRPT; ++r)
+            if (r < rpt) gram_wave(L, w, lane, x[r], gacc);
+        __syncthreads();
+        double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);   // [4][32][33] over the staging
+        const int qq = lane >> 4, l15 = lane & 15;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int rr = Mf<double>::crow(qq, g);
+            gw[w][rr][l15] = gacc[0][g];
+            gw[w][rr][16 + l15] = gacc[1][g];
+            gw[w][16 + l15][rr] = gacc[1][g];
+            gw[w][16 + rr][16 + l15] = gacc[2][g];
+        }
+        __syncthreads();
+        for (int el = tid; el < 1024; el += kCT) {
+            const int i = el >> 5, t = el & 31;
+            dst[(size_t)el * kCW] = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
+        }
+    };
+
+    // ---- pass 1 -------------------------------------------------------------
+    gram_partial(gp1 + wg);
+    CQR_STAMP(2);
+    if (tid == 0) ew[wg] = (double)e_w;
+    cluster_barrier(a.ctr, nwg, a.err);
+    CQR_STAMP(3);
+    __shared__ int ewl[kCW];
+    if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[tid] : INT_MIN;
+    __syncthreads();
+    int e = INT_MIN;
+    for (int k = 0; k < nwg; ++k) e = max(e, ewl[k]);
+    const bool zero = e == INT_MIN;   // the whole panel is zero: V = [I; 0], T = 0, R = 0
+
+    if (!zero) {
+        gram_reduce(L, gp1, ewl, nwg, e, true, gfin, wg, a.ctr, 2 * nwg, a.err);
+        CQR_STAMP(4);
+        __syncthreads();
+        if (w == 0) {
+            const bool good = chol_wave(L.g, L.r1, L.r1w, lane);
+            if (lane == 0) L.flags = good ? 0 : 1;
+        }
+        __syncthreads();
+        CQR_STAMP(5);
+        {
+        }
+        __syncthreads();
+        // Q1 = (P 2^-e) R1^-1
+#pragma unroll
+        for (int r = 0; r < kRPT; ++r) {
+            if (r < rpt) {
+                if (e_w != INT_MIN) {
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) x[r][t] = ldexp(x[r][t], e_w - e);
+                }
+                trsm_row(x[r], L.r1w);
+                if (rowid[r] < 0) {
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) x[r][t] = 0;
+                }
+            }
+        }
+        __syncthreads();
+        CQR_STAMP(6);
+        // ---- pass 2 ---------------------------------------------------------
+        gram_partial(gp2 + wg);
+        CQR_STAMP(7);
+        if (wg == 0 && tid < 32) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) q1top[tid * 32 + t] = x[0][t];
+        }
+        cluster_barrier(a.ctr, 3 * nwg, a.err);
+        CQR_STAMP(8);
+        gram_reduce(L, gp2, ewl, nwg, e, false, gfin, wg, a.ctr, 4 * nwg, a.err);
+        CQR_STAMP(9);
+        for (int el = tid; el < 1024; el += kCT) L.tq[el >> 5][el & 31] = q1top[el];
+        __syncthreads();
+        if (w == 0) {
+            // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8
+            // the Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle
+            // of E with half its diagonal) and its inverse I - U1 + O(E^2):
+            // both to working accuracy, without the 32-step factorization.
+            const int c = lane & 31;
+            double em = 0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) em = fmax(em, fabs(L.g[i][c] - (i == c ? 1.0 : 0.0)));
+            for (int o = 16; o >= 1; o >>= 1) em = fmax(em, __shfl_xor(em, o, 64));
+            const bool fast = em < 1e-8;   // wave-uniform
+            if (fast) {
+                if (lane < 32) {
+#pragma unroll
+                    for (int i = 0; i < 32; ++i) {
+                        const double u1 = i < c ? L.g[i][c] : (i == c ? 0.5 * (L.g[c][c] - 1.0) : 0.0);
+                        L.r2[i][c] = (i == c ? 1.0 : 0.0) + u1;
+                        L.r2w[i][c] = i == c ? 1.0 - u1 : u1;   // (reciprocal diagonal, first order)
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // Q_t = Q1_t (I - U1) (lane = row): y[t] = q[t] - sum_{k <= t} q[k] U1[k][t]
+                if (lane < 32) {
+                    typedef double d2 __attribute__((ext_vector_type(2)));
+                    double qv[32], y[32];
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) { qv[t] = L.tq[lane][t]; y[t] = qv[t]; }
+#pragma unroll
+                    for (int k = 0; k < 32; ++k) {
+                        d2 rr[16];
+#pragma unroll
+                        for (int p = k / 2; p < 16; ++p) rr[p] = *(const d2 *)&L.r2[k][2 * p];
+#pragma unroll
+                        for (int t = k; t < 32; ++t) {
+                            const double u = ((t & 1) ? rr[t >> 1].y : rr[t >> 1].x) - (t == k ? 1.0 : 0.0);
+                            y[t] = fma(-qv[k], u, y[t]);
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) L.tq[lane][t] = y[t];
+                }
+            } else {
+                const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
+                if (lane == 0 && !good) L.flags = 1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // Q_t = Q1_t R2^-1 (lane = row)
+                if (lane < 32) {
+                    double y[32];
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) y[t] = L.tq[lane][t];
+                    trsm_row(y, L.r2w);
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) L.tq[lane][t] = y[t];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // modified LU of Q_t - S = L U (lane r = row r; the pivot row is
+            // read back from LDS as 16-byte broadcasts, its owner writes it
+            // after each step)
+            {
+                typedef double d2 __attribute__((ext_vector_type(2)));
+                const int r = lane & 31;
+                double rv[32];
+#pragma unroll
+                for (int cc = 0; cc < 32; ++cc) rv[cc] = L.tq[r][cc];
+#pragma unroll
+                for (int jj = 0; jj < 32; ++jj) {
+                    d2 pr[16];
+#pragma unroll
+                    for (int p = jj / 2; p < 16; ++p) pr[p] = *(const d2 *)&L.tq[jj][2 * p];
+                    double piv = (jj & 1) ? pr[jj >> 1].y : pr[jj >> 1].x;
+                    const double sg = piv >= 0 ? -1.0 : 1.0;
+                    piv -= sg;                                    // |piv| >= 1
+                    double inv = __builtin_amdgcn_rcp(piv);
+                    inv = fma(inv, fma(-piv, inv, 1.0), inv);
+                    inv = fma(inv, fma(-piv, inv, 1.0), inv);
+                    if (r == jj) rv[jj] = piv;
+                    if (r > jj) {
+                        const double l = rv[jj] * inv;
+                        rv[jj] = l;
+#pragma unroll
+                        for (int cc = jj + 1; cc < 32; ++cc) rv[cc] = fma(-l, (cc & 1) ? pr[cc >> 1].y : pr[cc >> 1].x, rv[cc]);
+                    }
+                    if (lane == 0) L.sgn[jj] = sg;
+                    if (jj + 1 < 32) {
+                        if (lane == jj + 1) {
+#pragma unroll
+                            for (int p = (jj + 1) / 2; p < 16; ++p) *(d2 *)&L.tq[jj + 1][2 * p] = d2{rv[2 * p], rv[2 * p + 1]};
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                }
+                if (lane < 32) {
+#pragma unroll
+                    for (int cc = 0; cc < 32; ++cc) L.u[r][cc] = rv[cc];
+                }
+            }
+        }
+        __syncthreads();
+        CQR_STAMP(10);
+        if (L.flags && tid == 0 && wg == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w == 0) {
+            // M = U R2 (lane c = column c): M[i][c] = sum_{k >= i} U[i][k] R2[k][c]
+            const int c = lane & 31;
+            double r2c[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) r2c[k] = L.r2[k][c];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                double s = 0;
+#pragma unroll
+                for (int k = i; k < 32; ++k) s = fma(L.u[i][k], r2c[k], s);
+                if (lane < 32) L.mm[i][c] = i == c ? 1.0 / s : s;
+            }
+        } else if (w == 1 && wg == 0) {
+            // T (lane a = row a): T[a][k] = -U[a][k] s_k - sum_{a <= i < k} L[k][i] T[a][i]
+            const int ar = lane & 31;
+            double tr[32];
+            T *tout = (T *)a.tout;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                double s = ar <= k ? -L.u[ar][k] * L.sgn[k] : 0.0;
+#pragma unroll
+                for (int i = 0; i < k; ++i) s = fma(-L.u[k][i], tr[i], s);   // tr[i] = 0 for i < ar
+                tr[k] = s;
+                if (lane < 32) tout[ar * 32 + k] = (T)s;
+            }
+        } else if (w == 2 && wg == 0) {
+            // R = S R2 R1 2^e (lane c = column c) into the panel
+            const int c = lane & 31;
+            double r1c[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) r1c[k] = L.r1[k][c];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                double s = 0;
+#pragma unroll
+                for (int k = i; k < 32; ++k) s = fma(L.r2[i][k], r1c[k], s);
+                if (lane < 32) ap[(size_t)i * a.asi + (size_t)c * a.ast] = (T)ldexp(s * L.sgn[i], e);
+            }
+        }
+        __syncthreads();
+    } else {
+        // zero panel
+        for (int el = tid; el < 1024; el += kCT) {
+            const int i = el >> 5, t = el & 31;
+            L.u[i][t] = 0;
+            L.mm[i][t] = i == t ? 1.0 : 0.0;
+            if (wg == 0) {
+                ((T *)a.tout)[el] = (T)0;
+                ap[(size_t)i * a.asi + (size_t)t * a.ast] = (T)0;
+            }
+        }
+        __syncthreads();
+    }
+
+    CQR_STAMP(11);
+    // ---- V = Q1 M^-1 (rows >= 32), L (rows < 32); zeros below R --------------
+#pragma unroll
+    for (int r = 0; r < kRPT; ++r) {
+        const int i = rowid[r];
+        if (i < 0) continue;
+        T *vr = vd + (size_t)i * a.vsi, *vr2 = vd2 ? vd2 + (size_t)i * a.vsi2 : nullptr;
+        T *arow = ap + (size_t)i * a.asi;
+        const long vst = a.vst, vst2 = a.vst2, ast = a.ast;
+        if (i < 32) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) {
+                const T v = (T)(i > t ? L.u[i][t] : (i == t ? 1.0 : 0.0));
+                vr[t * vst] = v;
+                if (vr2) vr2[t * vst2] = v;
+            }
+        } else {
+            if (zero) {
+#pragma unroll
+                for (int t = 0; t < 32; ++t) x[r][t] = 0;
+            } else {
+                trsm_row(x[r], L.mm);
+            }
+            typedef typename G2<T>::v2 v2;
+            if (vst == 1) {
+#pragma unroll
+                for (int t = 0; t < 32; t += 2) *(v2 *)(vr + t) = v2{(T)x[r][t], (T)x[r][t + 1]};
+            } else {
+#pragma unroll
+                for (int t = 0; t < 32; ++t) vr[t * vst] = (T)x[r][t];
+            }
+            if (vr2) {
+                if (vst2 == 1) {
+#pragma unroll
+                    for (int t = 0; t < 32; t += 2) *(v2 *)(vr2 + t) = v2{(T)x[r][t], (T)x[r][t + 1]};
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 32; ++t) vr2[t * vst2] = (T)x[r][t];
+                }
+            }
+            if (ast == 1) {
+#pragma unroll
+                for (int t = 0; t < 32; t += 2) *(v2 *)(arow + t) = v2{(T)0, (T)0};
+            } else {
+#pragma unroll
+                for (int t = 0; t < 32; ++t) arow[t * ast] = (T)0;
+            }
+        }
+    }
+
+    // ---- exit: the last workgroup out resets the cluster counters -------------
+    __syncthreads();
+    CQR_STAMP(12);
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(a.ctr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nwg - 1) {
+            __hip_atomic_store(a.ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ==========================================================================
+// k_blkupd: C[r][c] -= sum_{k < 256} Lw[r][k] RwT[k][c] for r >= r0, c >= c0:
+// the block's delayed rank-256 update on the matrix cores.  Workgroup tile
+// 128 x 128 (4 waves of 64 x 64: 16 accumulator tiles of 16 x 16), K in
+// chunks of 16 through double-buffered LDS (Lw: pair-swizzled [kp][r][2];
+// RwT: [k][c] with a 144-element pitch), the C tile in the accumulators.
+// ==========================================================================
+constexpr int kGT = 256;
+constexpr int kGM = 128;
+constexpr int kGKC = 16;
+constexpr int kGBP = kGM + 16;
+
+struct GemmArgs {
+    void *C; long ldc;
+    int rows, cols;                 // extent of the updated region
+    const void *Lw; const void *RwT; long ldr;
+    int K;                          // 256
+    int tiles_c;                    // column tiles
+};
+
+template <typename T>
+struct GemmLds {
+    T a[2][kGKC * kGM];     // Lw tile, pair-swizzled
+    T b[2][kGKC * kGBP];    // RwT tile
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
+    typedef typename G2<T>::v2 v2;
+    typedef typename Mf<T>::v4 v4;
+    __shared__ GemmLds<T> L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l15 = lane & 15;
+    const int tr = blockIdx.x / a.tiles_c, tc = blockIdx.x % a.tiles_c;
+    const int r0 = tr * kGM, c0 = tc * kGM;
+    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+    T *C = (T *)a.C;
+    const T *Lw = (const T *)a.Lw;
+    const T *RwT = (const T *)a.RwT;
+
+    // C tile into the accumulators
+    v4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int r = r0 + wr + 16 * i + Mf<T>::crow(q, g), cc = c0 + wc + 16 * j + l15;
+                acc[i][j][g] = (r < a.rows && cc < a.cols) ? C[(size_t)r * a.ldc + cc] : (T)0;
+            }
+
+    // per chunk: Lw 128 x 16 (1024 granules), RwT 16 x 128 (1024 granules): 4 + 4 per thread
+    auto load = [&](int k0, v2 (&ga)[4], v2 (&gb)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + kGT * i;
+            const int r = e >> 3, kp = e & 7;
+            const int rg = r0 + r;
+            ga[i] = rg < a.rows ? *(const v2 *)(Lw + (size_t)rg * 256 + k0 + 2 * kp) : v2{(T)0, (T)0};
+            const int k = e >> 6, cp = e & 63;
+            const int cg = c0 + 2 * cp;
+            v2 v = {(T)0, (T)0};
+            if (cg < a.cols) {
+                const T *p = RwT + (size_t)(k0 + k) * a.ldr + cg;
+                if (cg + 1 < a.cols) v = *(const v2 *)p; else v.x = p[0];
+            }
+            gb[i] = v;
+        }
+    };
+    auto stage = [&](int buf, const v2 (&ga)[4], const v2 (&gb)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + kGT * i;
+            const int r = e >> 3, kp = e & 7;
+            // negated: the MFMA adds A B to the C tile
+            *(v2 *)&L.a[buf][2 * (kp * kGM + (r ^ kp))] = v2{-ga[i].x, -ga[i].y};
+            const int k = e >> 6, cp = e & 63;
+            *(v2 *)&L.b[buf][k * kGBP + 2 * cp] = gb[i];
+        }
+    };
+    const int nc = a.K / kGKC;
+    v2 ga[4], gb[4];
+    load(0, ga, gb);
+    for (int c = 0; c < nc; ++c) {
+        stage(c & 1, ga, gb);
+        lds_barrier();
+        if (c + 1 < nc) load((c + 1) * kGKC, ga, gb);
+#pragma unroll
+        for (int s = 0; s < kGKC / 4; ++s) {
+            const int k = 4 * s + q, kp = k >> 1, hf = k & 1;
+            T av[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wr + 16 * i + l15;
+                av[i] = L.a[c & 1][2 * (kp * kGM + (r ^ kp)) + hf];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = L.b[c & 1][k * kGBP + wc + 16 * j + l15];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int r = r0 + wr + 16 * i + Mf<T>::crow(q, g), cc = c0 + wc + 16 * j + l15;
+                if (r < a.rows && cc < a.cols) C[(size_t)r * a.ldc + cc] = acc[i][j][g];
+            }
+}
+
+}  // namespace blk
+
+// --------------------------------------------------------------------------
+// Host side
+// --------------------------------------------------------------------------
+using namespace blk;
+
+// Workspace of the blocked path (elements of T unless noted), carved from one
+// device buffer: Lw m x 256, RwT 256 x ldr, partials, Qp, virtual partials
+// and result, T/S factors, cluster scratch (doubles) and counters (ints).
+struct BlkLayout {
+    size_t lw, rwt, ub, part, vpart, vout, qp, tf, cws, ctr, total;
+    long ldr, mp;
+    int ksmax, cwg;
+};
+
+static BlkLayout blk_layout(int m, int n, size_t elem) {
+    BlkLayout L;
+    L.ldr = (n + 1) & ~1L;
+    L.mp = (std::max(m, n) + 1) & ~1L;
+    L.ksmax = 32;
+    L.cwg = kCW;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    L.lw = take((size_t)m * 256 * elem);
+    L.rwt = take((size_t)256 * L.ldr * elem);
+    L.ub = take((size_t)n * 32 * elem);
+    L.part = take((size_t)L.ksmax * 32 * L.mp * elem);
+    L.vpart = take((size_t)L.ksmax * 32 * 256 * elem);
+    L.vout = take((size_t)32 * 256 * elem);
+    L.qp = take((size_t)32 * L.mp * elem);
+    L.tf = take((size_t)8 * 1024 * elem);
+    L.cws = take(cqr_ws_doubles(L.cwg) * sizeof(double));
+    L.ctr = take(64 * sizeof(int));
+    L.total = off;
+    return L;
+}
+
+size_t blk_ws_bytes(int m, int n, size_t elem) { return blk_layout(m, n, elem).total; }
+
+int blk_columns(int n, int b) {
+    if (b != 32) return 0;
+    int k0 = 0;
+    while (n - k0 >= (NBMAX + 1) * 32) k0 += NBMAX * 32;
+    return k0;
+}
+
+template <typename T>
+static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
+                               long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
+                               int target, int *ksplit_out) {
+    RpArgs a;
+    a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
+    a.K = K; a.M = M;
+    a.mtiles = (M + kMT - 1) / kMT;
+    int ks = std::max(1, target / std::max(1, a.mtiles + 1));
+    ks = std::min(ks, std::max(1, K / 64));
+    ks = std::min(ks, Ly.ksmax);
+    a.kper = ((K + ks - 1) / ks + 7) / 8 * 8;
+    ks = (K + a.kper - 1) / a.kper;
+    a.ksplit = ks;
+    a.nvirt = vsrc ? ks : 0;
+    a.part = ws + Ly.part; a.mp = Ly.mp;
+    a.vpart = ws + Ly.vpart; a.vout = ws + Ly.vout;
+    a.counter = counter;
+    a.err = err;
+    *ksplit_out = ks;
+    dim3 grid(a.nvirt + a.mtiles * ks), block(kRT);
+    if (yp) hipLaunchKernelGGL((k_rpass<T, true>), grid, block, 0, s, a);
+    else    hipLaunchKernelGGL((k_rpass<T, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+// BRD_S1_STAMPS=1 (diagnostics): phase clocks of workgroup 0 of every k_cqr
+// launch, averaged and printed to stderr at the end of blk_ge2band.
+static unsigned long long *g_cqr_stamps = nullptr;
+static int g_cqr_calls = 0;
+
+template <typename T>
+static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
+                             long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
+                             hipStream_t s) {
+    CqrArgs a;
+    a.src = src; a.si = si; a.st = st; a.M = M;
+    a.vdst = vdst; a.vsi = vsi; a.vst = vst;
+    a.vdst2 = vdst2; a.vsi2 = vsi2; a.vst2 = vst2;
+    a.tout = tout; a.apan = apan; a.asi = asi; a.ast = ast;
+    int rpt = 1;
+    int nwg = (M + kCT * rpt - 1) / (kCT * rpt);
+    if (nwg > Ly.cwg) return hipErrorInvalidValue;
+    a.rpt = rpt;
+    a.ws = (double *)(ws + Ly.cws);
+    a.ctr = (int *)(ws + Ly.ctr);
+    a.err = err;
+    a.stamps = g_cqr_stamps ? g_cqr_stamps + 16 * g_cqr_calls : nullptr;
+    if (g_cqr_stamps && g_cqr_calls < 1023) ++g_cqr_calls;
+    hipLaunchKernelGGL((k_cqr<T>), dim3(nwg), dim3(kCT), 0, s, a);
+    return hipGetLastError();
+}
+
+// Blocked stage 1 over columns [0, kend) (kend = blk_columns(n, 32) > 0);
+// the caller finishes the remaining panels with the per-panel path.
+template <typename T>
+hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, int target, int *err) {
+    char *ws = (char *)wsv;
+    const BlkLayout Ly = blk_layout(m, n, sizeof(T));
+    const int kend = blk_columns(n, 32);
+    T *Lw = (T *)(ws + Ly.lw), *RwT = (T *)(ws + Ly.rwt), *Ub = (T *)(ws + Ly.ub);
+    T *tf = (T *)(ws + Ly.tf);   // T_j at tf + 1024 j, S_j at tf + 1024 (4 + j)
+    int *ctr = (int *)(ws + Ly.ctr);
+    const long ldr = Ly.ldr;
+    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);   // cluster / last-arriver counters
+    if (e != hipSuccess) return e;
+    const char *stenv = getenv("BRD_S1_STAMPS");
+    if (stenv && stenv[0] == '1') {
+        if (!g_cqr_stamps) hipMalloc(&g_cqr_stamps, 1024 * 16 * sizeof(unsigned long long));
+        hipMemsetAsync(g_cqr_stamps, 0, 1024 * 16 * sizeof(unsigned long long), s);
+        g_cqr_calls = 0;
+    }
+    int ks_x = 1;
+    for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
+        for (int j = 0; j < NBMAX; ++j) {
+            const int c = k0 + 32 * j;
+            const int mr = m - c;          // rows of the column panel
+            const int n2 = n - c - 32;     // columns right of it
+            T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
+            // ---- QR of the column panel --------------------------------------
+            if (j == 0) {
+                e = launch_cqr<T>(A + (size_t)c * lda + c, lda, 1, mr, Lw + (size_t)c * 256, 256, 1, nullptr, 0, 0, Tj,
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s);
+            } else {
+                PrepArgs p;
+                p.A = A; p.lda = lda; p.Lw = Lw; p.RwT = RwT; p.ldr = ldr;
+                p.part = ws + Ly.part; p.mp = Ly.mp; p.ksplit = ks_x;
+                p.G = ws + Ly.vout; p.Tm = tf + 1024 * (NBMAX + j - 1);
+                p.Qp = ws + Ly.qp; p.mq = Ly.mp;
+                p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
+                hipLaunchKernelGGL((k_prep_qr<T>), dim3((mr + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                e = launch_cqr<T>((const T *)(ws + Ly.qp), 32, 1, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s);
+            }
+            if (e != hipSuccess) return e;
+            // ---- Y pass + LQ of the row panel ----------------------------------
+            int ks_y = 1;
+            e = launch_rpass<T>(true, A + (size_t)c * lda + c + 32, lda, mr, n2, Lw + (size_t)c * 256 + 32 * j, 256,
+                                Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y);
+            if (e != hipSuccess) return e;
+            {
+                PrepArgs p;
+                p.A = A; p.lda = lda; p.Lw = Lw; p.RwT = RwT; p.ldr = ldr;
+                p.part = ws + Ly.part; p.mp = Ly.mp; p.ksplit = ks_y;
+                p.G = ws + Ly.vout; p.Tm = Tj;
+                p.Qp = ws + Ly.qp; p.mq = Ly.mp;
+                p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
+                hipLaunchKernelGGL((k_prep_lq<T>), dim3((n2 + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, n2, RwT + (size_t)(128 + 32 * j) * ldr + c + 32, 1, ldr,
+                              Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s);
+            if (e != hipSuccess) return e;
+            // ---- X pass ----------------------------------------------------------
+            e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,
+                                Ub + (size_t)(c + 32) * 32, 32, RwT + c + 32, ldr, ws, Ly, ctr + 16, err, s,
+                                target, &ks_x);
+            if (e != hipSuccess) return e;
+        }
+        // ---- block end: X_3, then the rank-256 update ---------------------------
+        const int k1 = k0 + NBMAX * 32;
+        {
+            PrepArgs p;
+            p.A = A; p.lda = lda; p.Lw = Lw; p.RwT = RwT; p.ldr = ldr;
+            p.part = ws + Ly.part; p.mp = Ly.mp; p.ksplit = ks_x;
+            p.G = ws + Ly.vout; p.Tm = tf + 1024 * (2 * NBMAX - 1);
+            p.Qp = ws + Ly.qp; p.mq = Ly.mp;
+            p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
+            hipLaunchKernelGGL((k_prep_qr<T>), dim3((m - k1 + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        {
+            GemmArgs g;
+            g.C = A + (size_t)k1 * lda + k1; g.ldc = lda;
+            g.rows = m - k1; g.cols = n - k1;
+            g.Lw = Lw + (size_t)k1 * 256; g.RwT = RwT + k1; g.ldr = ldr;
+            g.K = 256;
+            g.tiles_c = (g.cols + kGM - 1) / kGM;
+            const int tiles_r = (g.rows + kGM - 1) / kGM;
+            hipLaunchKernelGGL((k_blkupd<T>), dim3(tiles_r * g.tiles_c), dim3(kGT), 0, s, g);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (stenv && stenv[0] == '1' && g_cqr_stamps) {
+        std::vector<unsigned long long> h(1024 * 16);
+        hipStreamSynchronize(s);
+        hipMemcpy(h.data(), g_cqr_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+        double acc[16] = {0};
+        int cnt = 0;
+        for (int i = 0; i < g_cqr_calls; ++i) {
+            const unsigned long long *st = &h[16 * i];
+            if (!st[0] || !st[12]) continue;
+            ++cnt;
+            unsigned long long prev = st[0];
+            for (int k = 1; k <= 12; ++k) {
+                if (!st[k]) continue;
+                acc[k] += (double)(st[k] - prev);
+                prev = st[k];
+            }
+        }
+        fprintf(stderr, "k_cqr phases (clocks, mean over %d launches):", cnt);
+        for (int k = 1; k <= 12; ++k) fprintf(stderr, " %d:%.0f", k, cnt ? acc[k] / cnt : 0.0);
+        fprintf(stderr, "\n");
+    }
+    return hipSuccess;
+}
+
+template hipError_t blk_ge2band<double>(double *, int, int, long, void *, hipStream_t, int, int *);
+template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStream_t, int, int *);
+
+}  // namespace brd

@@ -247,7 +247,7 @@ int api_apply_target() {
     const int ov = g_ctx.overlap_cus;
     static const char *tenv = getenv("BRD_S1_TARGET");   // tuning: workgroups per apply launch
     if (tenv && atoi(tenv) > 0) return atoi(tenv);
-    return ov > 0 ? std::max(32, device_cus() - ov) : 256;
+    return ov > 0 ? std::max(32, device_cus() - ov) : device_cus();
 }
 
 // Least slabs per apply workgroup at tree level `level`.  Beside other work

@@ -1394,6 +1394,8 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
     a.K = K; a.M = M;
     a.mtiles = (M + kMT - 1) / kMT;
+    static const int rpx = getenv("BRD_BLK_RPX") ? std::max(1, atoi(getenv("BRD_BLK_RPX"))) : 1;   // tuning
+    target *= rpx;
     int ks = std::max(1, target / std::max(1, a.mtiles + 1));
     ks = std::min(ks, std::max(1, K / 64));
     ks = std::min(ks, Ly.ksmax);

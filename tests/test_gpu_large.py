@@ -98,6 +98,55 @@ def test_two_stage_at_bench_size(S, n, tname):
     assert float(torch.abs(d).max()) > 0
 
 
+def _bd_err(d, e, d0, e0):
+    import torch
+    got = torch.cat([d.abs(), e.abs()]).double()
+    ref = torch.cat([d0.abs(), e0.abs()]).double()
+    return float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n,tname", [(8192, "f64"), (8192, "f32"), (16384, "f64")])
+def test_compat_stage2_within_envelope_at_bench_size(S, n, tname):
+    """The stage 2 every bench line times (the reference's window geometry,
+    fast arithmetic) against the GPU exact-order sweep on the same band -- the
+    exact-order sweep is bit-identical to svd_parallel.h:640-695's operation
+    order (tests/test_gpu_parity.py pins it to the fixtures).  The compat
+    geometry is ill-conditioned (Stage 2), so the bound is the
+    reference's own sensitivity: how far its exact-order output moves when
+    the band is perturbed by one rounding error per element (two trials),
+    times 10, as in test_gpu_parity.py::_envelope."""
+    import torch
+    dt = torch.float64 if tname == "f64" else torch.float32
+    A = _rand(n, dt, seed=3 * n + (1 if tname == "f32" else 0))
+    S.ge2band(A, B)
+    band = A
+    del A
+    eps = float(torch.finfo(dt).eps)
+
+    def sweep(M, exact):
+        W = M.clone()
+        d, e = S.band2bd(W, B, exact_order=exact)
+        S.check_errors()
+        del W
+        return d.clone(), e.clone()
+
+    d0, e0 = sweep(band, True)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    env = 0.0
+    for _ in range(2):
+        p = band * (1 + eps * torch.randn(band.shape, dtype=dt, device="cuda", generator=g))
+        d1, e1 = sweep(p, True)
+        del p
+        env = max(env, _bd_err(d1, e1, d0, e0))
+    d, e = sweep(band, False)
+    assert bool(torch.isfinite(d).all()) and bool(torch.isfinite(e).all())
+    err = _bd_err(d, e, d0, e0)
+    assert env > 0
+    assert err <= 10 * env + 10 * eps, (err, env)
+
+
 @pytest.mark.parametrize("n", [1024, 8192])
 def test_two_stage_bitwise_reproducible(S, n):
     """Run twice, bitwise equal ('race detection'): stage 1

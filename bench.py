@@ -40,7 +40,7 @@ library's per-launch events (for the stage-1 apply stamped by the launch
 itself, hipExtLaunchKernel) for the dominant kernel's roofline object.  Also
 the CPU baseline: the reference's own tiled algorithm (built from its
 sources by oracle/Makefile) timed on this host at N = 320, 640, 1024 (about
-10-20 s), with a c N^3 fit extrapolated to the GPU problem size (labelled as
+10-20 s), with a c N^3 + d N^2 fit extrapolated to the GPU problem size (labelled as
 such).
 """
 from __future__ import annotations
@@ -140,8 +140,8 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
     the reference's sources by oracle/Makefile (README.md:32 flags minus
     -march=native), on n x n fp64 matrices uniform in [0,5), b = band, at each
     n in `sizes`.  OpenMP threads = the job's CPU share (OMP_NUM_THREADS, else
-    the affinity set).  A least-squares c n^3 fit over the samples gives the
-    EXTRAPOLATED time at the GPU problem size (not measured: ~45 min at 8192).
+    the affinity set).  A least-squares c n^3 + d n^2 fit over the samples gives the
+    EXTRAPOLATED time at the GPU problem size (not measured: ~15 min at 8192).
     Falls back to the single-threaded C oracle (kind "port")."""
     import ctypes
     import numpy as np
@@ -169,8 +169,15 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
             oracle.brd_p2(oracle.brd_p1(A, band), band)
         pts.append((n, time.perf_counter() - t0))
     n_s, dt = pts[-1]
-    c = sum(t * n ** 3 for n, t in pts) / sum(float(n) ** 6 for n, _ in pts)   # least squares t = c n^3
-    t_ext = c * float(gpu_n) ** 3
+    # t = c n^3 + d n^2, least squares in relative error: at these sizes the
+    # reference's time is dominated by its O(n^2) per-tile overheads and stage
+    # 2 (320 -> 1024: t ~ n^2.1), so a pure c n^3 fit through the small sizes
+    # overstates the large-n time ~2.5x (profiles/r02_cpu_baseline.json: this
+    # fit over 320..1024 predicts 38.2 s at 2048, measured 37.3 s)
+    M = np.array([[float(n) ** 3 / t, float(n) ** 2 / t] for n, t in pts])
+    coef = np.linalg.lstsq(M, np.ones(len(pts)), rcond=None)[0] if len(pts) >= 2 else np.array([dt / n_s ** 3, 0.0])
+    c, d = max(float(coef[0]), 0.0), max(float(coef[1]), 0.0)
+    t_ext = c * float(gpu_n) ** 3 + d * float(gpu_n) ** 2
     return {"value": round(8.0 / 3.0 * n_s ** 3 / dt / 1e9, 4), "unit": "GFLOP/s", "cores": used,
             "kind": kind, "sample": f"{n_s}x{n_s} fp64 two-stage reduction, b={band}, {dt:.2f} s, "
                                     f"{used} OpenMP threads",
@@ -178,7 +185,8 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
             "sizes_s": {str(n): round(t, 3) for n, t in pts},
             "extrapolated": {"n": gpu_n, "seconds": round(t_ext, 1),
                              "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_ext / 1e9, 4),
-                             "basis": "least-squares c*n^3 over the sampled sizes; NOT measured"}}
+                             "basis": "least-squares c*n^3 + d*n^2 (relative error) over the sampled sizes; "
+                                      "NOT measured"}}
 
 
 def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):
@@ -224,6 +232,64 @@ def apply_roofline(ap, dtype, n):
             "mfma_frac": round(tf / PEAK_TFLOPS[dtype], 4),
             "launches": ap["launches"], "avg_launch_us": round(ms * 1e3 / launches, 3),
             "flops_per_launch": round(ap["flops"] / launches)}
+
+
+def pmc_mfma(n: int, dtype: str, kernel_prefix: str):
+    """Counter-derived MFMA utilisation of a kernel from the committed
+    rocprofv3 PMC summary of this configuration (tools/pmc.sh's MFMA pass:
+    SQ_INSTS_VALU_MFMA_MOPS_F64/_F32 -- 512 flops per unit -- over
+    SQ_BUSY_CYCLES x CUs x the per-CU-cycle MFMA peak); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_n{n}_{dtype}.txt")))
+    if not files:
+        return None
+    for line in open(files[-1]):
+        if line.startswith("MFMA " + kernel_prefix):
+            try:
+                return float(line.split()[-1])
+            except ValueError:
+                return None
+    return None
+
+
+def blkupd_roofline(bu, dtype, n):
+    """Blocked stage 1's delayed trailing update (k_blkupd): C -= Lw RwT with
+    K = 256 (the 4 panels' left and right block reflectors of a block), one
+    read and one write of the trailing matrix per 128 columns against
+    2 x 256 flops per element -> 32 flop/B fp64, above the MFMA ridge
+    (78.6 TF / 8 TB/s = 9.8 flop/B): MFMA-bound."""
+    ms, launches = bu["ms"], max(bu["launches"], 1)
+    tf = bu["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    gbs = bu["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    tn = "double" if dtype == "f64" else "float"
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_blkupd<" + tn)
+    return {"kernel": "k_blkupd (stage-1 delayed rank-256 trailing update, MFMA)", "bound": "mfma",
+            "achieved": round(tf, 3), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_TFLOPS[dtype], 4),
+            "traffic": round(traffic) if traffic else None, "traffic_source": src,
+            "algorithmic_bytes_per_launch": round(bu["bytes"] / launches),
+            "flops_per_launch": round(bu["flops"] / launches),
+            "achieved_gbs": round(gbs, 1), "launches": bu["launches"],
+            "avg_launch_us": round(ms * 1e3 / launches, 3),
+            "mfma_util_counter": pmc_mfma(n, dtype, "k_blkupd")}
+
+
+def rpass_roofline(rp, dtype, n):
+    """Blocked stage 1's read passes (k_rpass: Y_j = A^T V_j and X_j = A U_j
+    per panel, the split-K partial sums): the trailing matrix read once per
+    pass, 2 x 32 flops per element -> 8 flop/B fp64: HBM-bound."""
+    ms, launches = rp["ms"], max(rp["launches"], 1)
+    gbs = rp["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    tf = rp["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    tn = "double" if dtype == "f64" else "float"
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_rpass<" + tn)
+    return {"kernel": "k_rpass (stage-1 read passes, MFMA)", "bound": "hbm", "achieved": round(gbs, 1),
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "traffic": round(traffic) if traffic else None, "traffic_source": src,
+            "algorithmic_bytes_per_launch": round(rp["bytes"] / launches),
+            "achieved_tflops": round(tf, 3), "launches": rp["launches"],
+            "avg_launch_us": round(ms * 1e3 / launches, 3),
+            "mfma_util_counter": pmc_mfma(n, dtype, "k_rpass")}
 
 
 def stage2_roofline(sw, n, b, dtype, steps):
@@ -512,6 +578,11 @@ def main():
     ap = S.profile_query("s1_apply")
     fa = S.profile_query("s1_factor")
     sw = S.profile_query("s2_sweep")
+    bu = S.profile_query("s1_blkupd")
+    rp = S.profile_query("s1_rpass")
+    cq = S.profile_query("s1_cqr")
+    pp = S.profile_query("s1_prep")
+    blocked = bu["launches"] > 0
 
     flops_per = 8.0 / 3.0 * n ** 3
     matrices = 1 if (world == 1 or dist_mode) else world   # matrices reduced per step, whole job
@@ -544,7 +615,9 @@ def main():
                                        "matrix i beside stage 1 of the next), fill and drain inside the timed region; "
                                        "per-reduction latency under overlap: latency_ms_per_reduction; one reduction "
                                        "at a time: one_at_a_time") if pipelined else "one reduction at a time"),
-                       "n": n, "band": b, "global_batch": matrices,
+                       "n": n, "band": b,
+                       # matrices in flight at once: one per lane in the stream
+                       "global_batch": matrices * (lanes if pipelined else 1),
                        "matrices_per_timed_region": matrices * args.steps,
                        "parallelism": (f"stage1 block-cyclic columns over {world} GPUs ({'RCCL' if args.comm == 'rccl' else 'host gloo'}), stage2 on rank "
                                        + ("(matrix index mod world)" if pipelined else "0")
@@ -559,11 +632,21 @@ def main():
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),
             "profiled_pass": "one reduction at a time" if serial_too else "as the timed steps",
-            "roofline": apply_roofline(ap, args.dtype, n),
+            # the dominant stage-1 kernel: the blocked path's delayed update
+            # (k_blkupd, MFMA-bound) when it ran, else the per-panel apply
+            "roofline": blkupd_roofline(bu, args.dtype, n) if blocked else apply_roofline(ap, args.dtype, n),
+            "roofline_read_pass": rpass_roofline(rp, args.dtype, n) if blocked else None,
+            "roofline_tail_apply": apply_roofline(ap, args.dtype, n) if blocked and ap["launches"] else None,
             "stage2": stage2_roofline(sw, n, b, args.dtype, args.steps),
-            "kernel_ms_per_step": {"s1_apply": round(ap["ms"] / args.steps, 3),
+            "kernel_ms_per_step": {"s1_blkupd": round(bu["ms"] / args.steps, 3),
+                                   "s1_rpass": round(rp["ms"] / args.steps, 3),
+                                   "s1_panel_cqr": round(cq["ms"] / args.steps, 3),
+                                   "s1_prep": round(pp["ms"] / args.steps, 3),
+                                   "s1_apply": round(ap["ms"] / args.steps, 3),
                                    "s1_factor": round(fa["ms"] / args.steps, 3),
                                    "s2_sweep": round(sw["ms"] / args.steps, 3)},
+            "stage1_path": "blocked (delayed two-sided update, brd_stage1_blk.hip) + per-panel tail" if blocked
+                           else "per-panel (brd_stage1.hip)",
         }
         if args.cpu_baseline == "auto":
             try:

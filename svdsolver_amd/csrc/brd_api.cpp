@@ -426,17 +426,18 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
 }
 
 // Blocked stage 1 (brd_stage1_blk.hip) for b = 32 -- the delayed two-sided
-// update -- over all but the last panels; BRD_S1_BLOCKED=0 keeps the
-// per-panel path throughout (A/B and parity against the per-panel kernels).
+// update -- over all but the last panels (the default); BRD_S1_BLOCKED=0
+// keeps the per-panel path throughout (A/B and parity against the per-panel
+// kernels).
 static bool blocked_enabled() {
     const char *env = getenv("BRD_S1_BLOCKED");   // read per call: tests switch it between calls
-    return env && env[0] == '1';
+    return !(env && env[0] == '0');
 }
 
 template <typename T>
 static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s, bool *used_blocked = nullptr) {
     const bool blk_ok = blocked_enabled() && b == 32 && lda % 2 == 0 && ((uintptr_t)A % 16) == 0;
-    const int kend = blk_ok ? blk_columns(n, b) : 0;
+    const int kend = blk_ok ? blk_columns(m, n, b) : 0;
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));
     if (kend > 0) need = std::max(need, blk_ws_bytes(m, n, sizeof(T)));
@@ -490,6 +491,17 @@ void api_prof_end(void *h, hipStream_t s) {
     hipEventRecord(p->b, s);
     g_ctx.pending.push_back(*p);
     delete p;
+}
+// Launch-mode profiling for kernels launched outside a ProfScope (the blocked
+// stage 1): two events the caller hands to hipExtLaunchKernel, queued for
+// prof_drain.  False (no events) when profiling is off.
+bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b) {
+    if (!g_ctx.prof) return false;
+    Pending p{kind, get_event(), get_event(), flops, bytes};
+    *a = p.a;
+    *b = p.b;
+    g_ctx.pending.push_back(p);
+    return true;
 }
 void api_lock() { g_ctx.mu.lock(); }
 void api_unlock() { g_ctx.mu.unlock(); }

@@ -65,7 +65,7 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
 // remaining panels with the per-panel path.  err: device error word (2:
 // cluster barrier timeout, 3: CholeskyQR breakdown).
 size_t blk_ws_bytes(int m, int n, size_t elem);
-int blk_columns(int n, int b);
+int blk_columns(int m, int n, int b);
 template <typename T>
 hipError_t blk_ge2band(T *A, int m, int n, long lda, void *ws, hipStream_t s, int target, int *err);
 
@@ -89,6 +89,7 @@ int api_min_run(int level);                        // least slabs per apply work
 bool api_overlap_active();                         // brd_set_overlap reservation in force
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
+bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b);
 // Profiling with kernel-bracketing events: a ProfScope in "launch" mode arms a
 // pair of events that the NEXT stage-1 launch takes (hipExtLaunchKernel
 // records them at the dispatch's start and end, the timestamps rocprofv3

@@ -84,7 +84,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // their partials into vout in fixed order (deterministic).
 // ==========================================================================
 constexpr int NBMAX = 4;    // panels per block (Lw / RwT hold 2 NBMAX 32 = 256 vectors)
-constexpr int kRT = 256;    // threads (4 waves)
+constexpr int kRT = 512;    // threads: 4 column waves x 2 halves of the workgroup's K range
 constexpr int kWM = 64;     // m per wave
 constexpr int kMT = 256;    // m per workgroup
 constexpr int kSU = 8;      // K steps in flight (Y); X: kSU / 2 step pairs
@@ -99,15 +99,15 @@ struct RpArgs {
     void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
     void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
     void *vout;                     // virtual result [32][256] / [256][32]
-    int *counter;                   // [0]: virtual-tile barrier, [1]: exit (0 between launches)
+    int *counter;                   // virtual workgroups finished (0 between launches)
     int *err;
 };
 
 template <typename T, bool YP>
-__global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
+__global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a) {
     typedef typename G2<T>::v2 v2;
     typedef typename Mf<T>::v4 v4;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, kh = tid >> 8;
     const int q = lane >> 4, l15 = lane & 15;
     const int bid = blockIdx.x;
     const bool virt = bid < a.nvirt;
@@ -120,7 +120,11 @@ __global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
     if (virt) { S = (const T *)a.vsrc; ld = a.vld; M = kMT; }
     else      { S = (const T *)a.src + (YP ? (long)mx * kMT : (long)mx * kMT * a.ld); ld = a.ld; M = min(kMT, a.M - mx * kMT); }
     const T *B = (const T *)a.bsrc;
-    const int kbeg = ks * a.kper, kend = min(a.K, kbeg + a.kper);
+    // waves w and w + 4 take the two halves of the workgroup's K range (in
+    // whole 8-row step pairs) and meet in LDS: two waves per SIMD in flight
+    const int kb0 = ks * a.kper, ke0 = min(a.K, kb0 + a.kper);
+    const int khalf = ke0 > kb0 ? ((ke0 - kb0 + 15) / 16) * 8 : 0;
+    const int kbeg = kh ? min(ke0, kb0 + khalf) : kb0, kend = kh ? ke0 : min(ke0, kb0 + khalf);
     const int mb = kWM * w;
     v4 acc[8];
 #pragma unroll
@@ -210,6 +214,23 @@ __global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
         }
     }
 
+    // ---- the second half's sums into the first half's, fixed order ----------
+    {
+        __shared__ T red[4][32][64];
+        if (kh) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) red[w][4 * i + g][lane] = acc[i][g];
+        }
+        __syncthreads();
+        if (!kh) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) acc[i][g] += red[w][4 * i + g][lane];
+        }
+    }
     // ---- partials ----------------------------------------------------------
     T *out;
     long mp;
@@ -219,6 +240,7 @@ __global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
+            if (kh) break;
             const int r = Mf<T>::crow(q, g);
             if (YP) {
                 const int h = i >> 2, p = (i >> 1) & 1, e = i & 1;
@@ -230,45 +252,22 @@ __global__ void __launch_bounds__(kRT, 2) k_rpass(RpArgs a) {
                 if (m < M) out[(size_t)m * 32 + t] = acc[i][g];
             }
         }
-    if (!virt) return;
+}
 
-    // ---- virtual tile: meet, then each workgroup sums one slice ---------------
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        long spins = 0;
-        while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.nvirt) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1L << 26)) { __hip_atomic_store(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const T *vp = (const T *)a.vpart;
-    const int per = (32 * kMT + a.nvirt - 1) / a.nvirt;
-    const int e0 = ks * per, e1 = min(32 * kMT, e0 + per);
-    for (int e = e0 + tid; e < e1; e += kRT) {
-        T v[32];
+// The virtual tile's split-K partials summed in fixed order (one element per
+// thread, every partial's load in flight at once): a kernel of its own, so
+// no workgroup of the read pass waits for another.
+template <typename T>
+__global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt) {
+    const int e = blockIdx.x * 256 + threadIdx.x;   // < 32 kMT
+    T v[32];
 #pragma unroll
-        for (int k = 0; k < 32; ++k) v[k] = k < a.nvirt ? vp[(size_t)k * 32 * kMT + e] : (T)0;
-        T s = v[0];
+    for (int k = 0; k < 32; ++k) v[k] = vpart[(size_t)min(k, nvirt - 1) * 32 * kMT + e];
+    T s = v[0];
 #pragma unroll
-        for (int k = 1; k < 32; ++k)
-            if (k < a.nvirt) s += v[k];
-        ((T *)a.vout)[e] = s;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(a.counter + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == a.nvirt - 1) {
-            __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.counter + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    for (int k = 1; k < 32; ++k)
+        if (k < nvirt) s += v[k];
+    vout[e] = s;
 }
 
 // ==========================================================================
@@ -631,23 +630,33 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 }
 
 // ==========================================================================
-// k_cqr: QR of a tall M x 32 panel as a Householder block reflector, by a
-// cluster of workgroups (one thread per row, up to kRPT rows per thread):
-//   Gram G1 = P^T P (power-of-two prescaled per workgroup, summed in fixed
-//   order after a cluster barrier), Cholesky R1, Q1 = P R1^-1, Gram G2
-//   (workgroup 0 also publishes Q1's top 32 rows), second barrier; then
-//   every workgroup, redundantly: Cholesky R2, the top block Q_t = Q1_t R2^-1,
-//   its modified LU Q_t - S = L U (s_j = -sign of the pivot: Ballard et al.
-//   2015), M = U R2, and V = Q1 M^-1 for its rows (rows < 32: L).  Workgroup
-//   0 also forms T = -U S L^-T and R = S R2 R1 and writes them.  Two cluster
-//   barriers per panel; all arithmetic in fp64.
-// A Cholesky pivot that is not positive or below 1e-7 x the largest (panel
-// condition number beyond ~1e7, where CholeskyQR2 loses orthogonality) sets
-// the error word (3).
+// k_cqr_*: QR of a tall M x 32 panel P as an orthogonal block reflector
+// Q' = I - V T V^T with Q'^T P = [R; 0], by nwg = ceil(M / 256) workgroups,
+// one thread per row, in three kernels (the kernel boundaries are the
+// panel-wide synchronisations, so no workgroup ever waits for another and
+// nothing requires co-residency -- several lanes' kernels share the chip):
+//   k_cqr_gram  per workgroup: the rows, their largest power-of-two exponent,
+//               the Gram partial of the prescaled rows
+//   k_cqr_q1    every workgroup: the partials summed in fixed order (each
+//               rescaled to the panel's exponent), R1 = chol(G1) (redundantly,
+//               wave 0), Q1 = P 2^-e R1^-1 for its rows (to the workspace),
+//               the Gram partial of Q1
+//   k_cqr_v     every workgroup: G2 = Q1^T Q1, R2 = chol(G2) (first order
+//               when G2 = I + E with |E| < 1e-8), V = Q = Q1 R2^-1 for its
+//               rows >= 32 (basis-kernel form: V = Q - [S; 0]); workgroup 0:
+//               the modified LU of the top block, Q_t - S = L U (s_j = -sign
+//               of the pivot, Ballard et al. 2015), V's top rows Q_t - S,
+//               T = -S (U^-1 L^-1)^T and the band block R = S R2 R1 2^e.
+// (Q' is orthogonal and Q' [S; 0] = Q for any sign matrix S with W_t = Q_t - S
+// invertible -- the basis-kernel representation of Sun and Bischof; the
+// modified LU's sign choice keeps W_t well conditioned, as in the Householder
+// reconstruction.)  All arithmetic in fp64.  A Cholesky pivot that is not
+// positive or below 1e-7 x the largest (panel condition number beyond ~1e7,
+// where CholeskyQR2 loses orthogonality) sets the error word (3).
 // ==========================================================================
 constexpr int kCT = 256;
-constexpr int kRPT = 1;
 constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
+constexpr int kCW = 64;   // most workgroups per panel (M <= kCW kCT rows)
 
 struct CqrArgs {
     const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
@@ -656,56 +665,37 @@ struct CqrArgs {
     void *vdst2; long vsi2, vst2;     // optional second copy of V (null: none)
     void *tout;                       // T (32 x 32)
     void *apan; long asi, ast;        // the panel in A: (i, t)
-    int rpt;                          // rows per thread
-    double *ws;                       // cluster scratch (cqr_ws_doubles)
-    int *ctr;                         // [0]: barrier, [1]: exit
+    double *ws;                       // scratch (cqr_ws_doubles)
     int *err;
-    unsigned long long *stamps;       // diagnostics (BRD_S1_STAMPS): workgroup 0's phase clocks, or null
 };
 
-// scratch (doubles): the two Gram passes' partials (separate: a fast
-// workgroup writes its second partial while others still sum the first),
-// per-workgroup exponents, Q1's top block
-__host__ __device__ constexpr size_t cqr_ws_doubles(int nwg) { return (size_t)2 * 1024 * 64 + (size_t)nwg + 2048 + 64; }
-
-__device__ __forceinline__ bool cluster_barrier(int *ctr, int target, int *err) {
-    // every workgroup: all threads' stores drained, then one arrival
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ int s_ok;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        long spins = 0;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1L << 26)) { ok = 0; __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
+// scratch (doubles): the two Gram passes' partials [kCW][1024] each, the
+// per-workgroup exponents, R1, and Q1's rows [kCW kCT][32]
+__host__ __device__ constexpr size_t cqr_ws_doubles() {
+    return (size_t)2 * 1024 * kCW + kCW + 1024 + (size_t)kCW * kCT * 32;
 }
+struct CqrWs {
+    double *gp1, *gp2, *ew, *r1, *q1;
+    __device__ explicit CqrWs(double *ws)
+        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 2048 * kCW), r1(ws + 2048 * kCW + kCW),
+          q1(ws + 2048 * kCW + kCW + 1024) {}
+};
 
 struct CqrLds {
     // the 32 x 32 matrices first: their LDS addresses fit the 16-bit offset field
     double g[32][kSP];       // reduced Gram
     double r1[32][kSP];      // R1 (upper, row-major)
     double r2[32][kSP];      // R2
-    double u[32][kSP];       // LU of the top block: U (upper) and L (strict lower)
-    double mm[32][kSP];      // M = U R2 with the reciprocal diagonal (trsm_row's form)
-    double tq[32][kSP];      // Q1's / Q's top block
-    double r1w[32][kSP];     // R1, R2 in trsm_row's form
-    double r2w[32][kSP];
+    double u[32][kSP];       // U of the top block's LU (upper)
+    double mm[32][kSP];      // L^-1
+    double tq[32][kSP];      // Q's top block; then L (strict lower)
+    double r1w[32][kSP];     // R1 in trsm_row's form; then U^-1
+    double r2w[32][kSP];     // R2^-1 (first order) or R2 in trsm_row's form
     double sgn[32];
-    double emax;
+    double scl[kCW];         // per-partial scale factors of the Gram sum
     int e_w;
     int flags;
-    double q[4][64][33];     // per-wave staging of 64 rows (Gram); then per-wave Gram partials
+    double q[4][64][33];     // per-wave staging of 64 rows (Gram, coalesced stores); per-wave Gram partials
 };
 
 __device__ __forceinline__ double rdl(double v, int l) {   // lane l's value, wave-uniform
@@ -785,6 +775,51 @@ __device__ __forceinline__ bool chol_wave(const double (&G)[32][kSP], double (&R
     return ok;
 }
 
+// Modified LU of Q_t - S = L U (Ballard et al. 2015: s_j = -sign of the
+// pivot, so every pivot has |.| >= 1) by one wave, lane r holding row r
+// (lanes 32-63 mirror).  The pivot row is lane jj's registers, broadcast by
+// readlanes (measured: 27 k clocks for the 32 steps; the same loop with the
+// pivot row published in LDS by its owner and read back as 16-byte
+// broadcasts took 34 k).  On return lane r's rv holds row r of L (strict
+// lower, unit diagonal implied) and U (upper); sgn[j] = s_j (LDS).
+__device__ __forceinline__ void lu_wave(double (&rv)[32], double *sgn, int lane) {
+    const int r = lane & 31;
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) {
+        double piv = rdl(rv[jj], jj);
+        const double sg = piv >= 0 ? -1.0 : 1.0;
+        piv -= sg;                                    // |piv| >= 1
+        double inv = __builtin_amdgcn_rcp(piv);
+        inv = fma(inv, fma(-piv, inv, 1.0), inv);
+        inv = fma(inv, fma(-piv, inv, 1.0), inv);
+        if (lane == 0) sgn[jj] = sg;
+        const bool below = r > jj;
+        const double l = rv[jj] * inv;
+        const double lb = below ? l : 0.0;   // rows <= jj: an exact no-op update, no selects
+#pragma unroll
+        for (int cc = jj + 1; cc < 32; ++cc) {
+            const double u = rdl(rv[cc], jj);
+            rv[cc] = fma(-lb, u, rv[cc]);
+            if (((cc - jj) & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bounds live scalar registers
+        }
+        rv[jj] = below ? l : (r == jj ? piv : rv[jj]);
+    }
+}
+
+// One 16 x 16 tile (ti, tj) of C = A B for 32 x 32 matrices in LDS, K range
+// [k0, 32) (k0 a multiple of 4: triangular operands skip their zero blocks).
+__device__ __forceinline__ Mf<double>::v4 tile_mm(const double (&A)[32][kSP], const double (&B)[32][kSP], int ti, int tj,
+                                                 int lane, int k0, int k1) {
+    const int q = lane >> 4, l15 = lane & 15;
+    Mf<double>::v4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = k0; k < k1; k += 4) acc = Mf<double>::mma(A[16 * ti + l15][k + q], B[k + q][16 * tj + l15], acc);
+    return acc;
+}
+__device__ __forceinline__ void tile_store(double (&C)[32][kSP], const Mf<double>::v4 &t, int ti, int tj, int lane) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) C[16 * ti + Mf<double>::crow(lane >> 4, g)][16 * tj + (lane & 15)] = t[g];
+}
+
 // x <- x R^-1, right-looking.  Rw: R (upper) with the reciprocal of its
 // diagonal in place of the diagonal, in LDS.  Row k + 1 of Rw is read (as
 // 16-byte pairs, a wave-uniform address: one LDS broadcast per pair) while
@@ -813,412 +848,399 @@ __device__ __forceinline__ void trsm_row(double (&x)[32], const double (&Rw)[32]
     }
 }
 
-// fixed-order sum of the cluster's Gram partials into L.g: 4 entries per
-// thread, all (<= kCW) partials of an entry loaded at once
-constexpr int kCW = 64;   // most workgroups per cluster (M <= kCW kCT rows)
-// Two-level fixed-order sum of the cluster's Gram partials: workgroup wg
-// sums its slice of the 1024 entries over all partials into gfin, a cluster
-// barrier, then every workgroup reads gfin (8 KB) into L.g.
-__device__ __forceinline__ void gram_reduce(CqrLds &L, const double *gp, const int *ewl, int nwg, int e, bool scaled,
-                                            double *gfin, int wg, int *ctr, int target, int *err) {
-    // gp: [1024][kCW] (entry-major: one entry's partials are contiguous)
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    const int tid = threadIdx.x;
-    const int per = (1024 + nwg - 1) / nwg;
-    for (int el = wg * per + tid; el < min(1024, (wg + 1) * per); el += kCT) {
-        d2 v[kCW / 2];
+// x <- x Ri for an upper-triangular Ri in LDS (all products independent:
+// x[t] = sum_{k <= t} x[k] Ri[k][t], k ascending).
+__device__ __forceinline__ void umul_row(double (&x)[32], const double (&Ri)[32][kSP]) {
+    double acc[32];
 #pragma unroll
-        for (int k = 0; k < kCW / 2; ++k) v[k] = *(const d2 *)(gp + (size_t)el * kCW + 2 * k);
-        double s = 0;
+    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
 #pragma unroll
-        for (int k = 0; k < kCW; ++k) {
-            double t = (k & 1) ? v[k >> 1].y : v[k >> 1].x;
-            if (scaled) {
-                const int ek = ewl[k];
-                t = ek != INT_MIN ? ldexp(t, 2 * (ek - e)) : 0.0;
-            }
-            s += k < nwg ? t : 0.0;
-        }
-        gfin[el] = s;
+    for (int k = 0; k < 32; ++k) {
+        d2v rr[16];
+#pragma unroll
+        for (int p = k / 2; p < 16; ++p) rr[p] = *(const d2v *)&Ri[k][2 * p];
+#pragma unroll
+        for (int t = k; t < 32; ++t) acc[t] = fma(x[k], (t & 1) ? rr[t >> 1].y : rr[t >> 1].x, acc[t]);
     }
-    cluster_barrier(ctr, target, err);
-    for (int el = tid; el < 1024; el += kCT) L.g[el >> 5][el & 31] = gfin[el];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) x[t] = acc[t];
 }
 
-#define CQR_STAMP(k)                                                                      \
-    do {                                                                                  \
-        if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[k] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
+// The cluster's Gram partials (workgroup-major [nwg][1024]) summed by every
+// workgroup on its own, in fixed order (deterministic), scaled by the
+// per-partial powers of two scl[k]: one cluster barrier per Gram instead of a
+// slice-sum, a second barrier and a read-back.
+__device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg) {
+    const int tid = threadIdx.x;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < nwg; k0 += 8) {
+        double v[8][4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int kc = min(k0 + k, nwg - 1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[k][u] = gp[(size_t)kc * 1024 + tid + kCT * u];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double sk = k0 + k < nwg ? scl[k0 + k] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = fma(sk, v[k][u], acc[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int el = tid + kCT * u;
+        L.g[el >> 5][el & 31] = acc[u];
+    }
+}
 
+// this thread's row of P (zeros past M), as doubles
 template <typename T>
-__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr(CqrArgs a) {
-    __shared__ CqrLds L;
-    CQR_STAMP(0);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nwg = gridDim.x, wg = blockIdx.x;
-    const int rpt = a.rpt;
-    double *gp1 = a.ws;                               // [1024][kCW] Gram partials, entry-major
-    double *gp2 = a.ws + (size_t)1024 * kCW;          // [1024][kCW]
-    double *ew = a.ws + (size_t)2048 * kCW;           // [nwg] exponents (as doubles)
-    double *q1top = ew + nwg;                         // [32][32]
-    double *gfin = q1top + 1024;                      // [32][32] the reduced Gram
+__device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x)[32]) {
     const T *src = (const T *)a.src;
-    T *ap = (T *)a.apan;
-    T *vd = (T *)a.vdst;
-    T *vd2 = (T *)a.vdst2;
-
-    // ---- rows into registers ------------------------------------------------
-    double x[kRPT][32];
-    int rowid[kRPT];
-    double amax = 0;
+    const T *srow = src + (size_t)(i < a.M ? i : 0) * a.si;
+    if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
+        typedef typename G2<T>::v2 v2;
 #pragma unroll
-    for (int r = 0; r < kRPT; ++r) {
-        const int i = (wg * rpt + r) * kCT + tid;
-        rowid[r] = (r < rpt && i < a.M) ? i : -1;
-        const T *srow = src + (size_t)(rowid[r] >= 0 ? i : 0) * a.si;
-        if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
-            typedef typename G2<T>::v2 v2;
-#pragma unroll
-            for (int t = 0; t < 32; t += 2) {
-                const v2 v = *(const v2 *)(srow + t);
-                x[r][t] = (double)v.x;
-                x[r][t + 1] = (double)v.y;
-            }
-        } else {
-            const long st = a.st;
-#pragma unroll
-            for (int t = 0; t < 32; ++t) x[r][t] = (double)srow[t * st];
+        for (int t = 0; t < 32; t += 2) {
+            const v2 v = *(const v2 *)(srow + t);
+            x[t] = (double)v.x;
+            x[t + 1] = (double)v.y;
         }
+    } else {
+        const long st = a.st;
 #pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            if (rowid[r] < 0) x[r][t] = 0.0;
-            amax = fmax(amax, fabs(x[r][t]));
-        }
+        for (int t = 0; t < 32; ++t) x[t] = (double)srow[t * st];
     }
-    // workgroup max -> power-of-two exponent (frexp: amax = f 2^e, 0.5 <= f < 1)
-    {
-        double m = amax;
-        for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-        if (tid == 0) L.e_w = INT_MIN;
-        __syncthreads();
-        if (lane == 0) {
-            int e = INT_MIN;
-            if (m > 0) frexp(m, &e);
-            atomicMax(&L.e_w, e);
-        }
-        __syncthreads();
+    if (i >= a.M) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) x[t] = 0.0;
     }
-    const int e_w = L.e_w;
-    CQR_STAMP(1);
-    if (e_w != INT_MIN) {
+}
+
+// Gram partial of the workgroup's rows (one per thread) -> dst (1024 doubles):
+// the four waves' partials summed in fixed order
+__device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32], double *dst) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    double gacc[3][4] = {};
+    gram_wave(L, w, lane, x, gacc);
+    __syncthreads();
+    double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);   // [4][32][33] over the staging
+    const int qq = lane >> 4, l15 = lane & 15;
 #pragma unroll
-        for (int r = 0; r < kRPT; ++r)
-#pragma unroll
-            for (int t = 0; t < 32; ++t) x[r][t] = ldexp(x[r][t], -e_w);
+    for (int g = 0; g < 4; ++g) {
+        const int rr = Mf<double>::crow(qq, g);
+        gw[w][rr][l15] = gacc[0][g];
+        gw[w][rr][16 + l15] = gacc[1][g];
+        gw[w][16 + l15][rr] = gacc[1][g];
+        gw[w][16 + rr][16 + l15] = gacc[2][g];
     }
+    __syncthreads();
+    for (int el = tid; el < 1024; el += kCT) {
+        const int i = el >> 5, t = el & 31;
+        dst[el] = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
+    }
+}
 
-    // Gram partial of the rows in registers -> dst (1024 doubles)
-    auto gram_partial = [&](double *dst) {
-        double gacc[3][4] = {};
-#pragma unroll
-        for (int r = 0; r < kRPT; ++r)
-            if (r < rpt) gram_wave(L, w, lane, x[r], gacc);
-        __syncthreads();
-        double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);   // [4][32][33] over the staging
-        const int qq = lane >> 4, l15 = lane & 15;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int rr = Mf<double>::crow(qq, g);
-            gw[w][rr][l15] = gacc[0][g];
-            gw[w][rr][16 + l15] = gacc[1][g];
-            gw[w][16 + l15][rr] = gacc[1][g];
-            gw[w][16 + rr][16 + l15] = gacc[2][g];
-        }
-        __syncthreads();
-        for (int el = tid; el < 1024; el += kCT) {
-            const int i = el >> 5, t = el & 31;
-            dst[(size_t)el * kCW] = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
-        }
-    };
-
-    // ---- pass 1 -------------------------------------------------------------
-    gram_partial(gp1 + wg);
-    CQR_STAMP(2);
-    if (tid == 0) ew[wg] = (double)e_w;
-    cluster_barrier(a.ctr, nwg, a.err);
-    CQR_STAMP(3);
+// the panel's exponent e (INT_MIN: the panel is zero) and the partials' scale
+// factors 2^(2 (e_k - e)) into L.scl
+__device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg, bool ones) {
+    const int tid = threadIdx.x;
     __shared__ int ewl[kCW];
     if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[tid] : INT_MIN;
     __syncthreads();
     int e = INT_MIN;
     for (int k = 0; k < nwg; ++k) e = max(e, ewl[k]);
-    const bool zero = e == INT_MIN;   // the whole panel is zero: V = [I; 0], T = 0, R = 0
+    if (tid < kCW) L.scl[tid] = ones ? 1.0 : ((tid < nwg && ewl[tid] != INT_MIN) ? ldexp(1.0, 2 * (ewl[tid] - e)) : 0.0);
+    __syncthreads();
+    return e;
+}
 
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
+    __shared__ CqrLds L;
+    const int tid = threadIdx.x, lane = tid & 63, wg = blockIdx.x;
+    CqrWs W(a.ws);
+    double x[32];
+    cqr_load_row<T>(a, wg * kCT + tid, x);
+    double m = 0;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) m = fmax(m, fabs(x[t]));
+    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) L.e_w = INT_MIN;
+    __syncthreads();
+    if (lane == 0) {
+        int e = INT_MIN;
+        if (m > 0) frexp(m, &e);
+        atomicMax(&L.e_w, e);
+    }
+    __syncthreads();
+    const int e_w = L.e_w;
+    if (e_w != INT_MIN) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e_w);
+    }
+    cqr_gram_partial(L, x, W.gp1 + (size_t)wg * 1024);
+    if (tid == 0) W.ew[wg] = (double)e_w;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
+    __shared__ CqrLds L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
+    CqrWs W(a.ws);
+    if (tid == 0) L.flags = 0;
+    const int e = cqr_exponent(L, W.ew, nwg, false);
+    const int i = wg * kCT + tid;
+    double x[32];
+    if (e == INT_MIN) {   // zero panel: k_cqr_v writes V = [I; 0], T = 0, R = 0
+        return;
+    }
+    gram_sum_all(L, W.gp1, L.scl, nwg);
+    __syncthreads();
+    if (w == 0) {
+        const bool good = chol_wave(L.g, L.r1, L.r1w, lane);
+        if (lane == 0 && !good) L.flags = 1;
+    }
+    __syncthreads();
+    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg == 0) {
+        for (int el = tid; el < 1024; el += kCT) W.r1[el] = L.r1[el >> 5][el & 31];
+    }
+    // Q1 = (P 2^-e) R1^-1
+    cqr_load_row<T>(a, i, x);
+#pragma unroll
+    for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e);
+    trsm_row(x, L.r1w);
+    if (i >= a.M) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) x[t] = 0.0;
+    }
+    {
+        d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
+    }
+    cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr_v(CqrArgs a) {
+    __shared__ CqrLds L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
+    CqrWs W(a.ws);
+    if (tid == 0) L.flags = 0;
+    const int e = cqr_exponent(L, W.ew, nwg, true);
+    const bool zero = e == INT_MIN;   // V = [I; 0], T = 0, R = 0
+    const int i = wg * kCT + tid;
+    T *ap = (T *)a.apan;
+    T *vd = (T *)a.vdst;
+    T *vd2 = (T *)a.vdst2;
+    double x[32];
     if (!zero) {
-        gram_reduce(L, gp1, ewl, nwg, e, true, gfin, wg, a.ctr, 2 * nwg, a.err);
-        CQR_STAMP(4);
+        gram_sum_all(L, W.gp2, L.scl, nwg);
         __syncthreads();
-        if (w == 0) {
-            const bool good = chol_wave(L.g, L.r1, L.r1w, lane);
-            if (lane == 0) L.flags = good ? 0 : 1;
-        }
-        __syncthreads();
-        CQR_STAMP(5);
+        // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
+        // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
+        // half its diagonal) and its inverse I - U1 + O(E^2): both to working
+        // accuracy, without the 32-step factorization.  Every wave decides
+        // (the same reads, the same result).
+        bool fast;
         {
-        }
-        __syncthreads();
-        // Q1 = (P 2^-e) R1^-1
-#pragma unroll
-        for (int r = 0; r < kRPT; ++r) {
-            if (r < rpt) {
-                if (e_w != INT_MIN) {
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) x[r][t] = ldexp(x[r][t], e_w - e);
-                }
-                trsm_row(x[r], L.r1w);
-                if (rowid[r] < 0) {
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) x[r][t] = 0;
-                }
-            }
-        }
-        __syncthreads();
-        CQR_STAMP(6);
-        // ---- pass 2 ---------------------------------------------------------
-        gram_partial(gp2 + wg);
-        CQR_STAMP(7);
-        if (wg == 0 && tid < 32) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) q1top[tid * 32 + t] = x[0][t];
-        }
-        cluster_barrier(a.ctr, 3 * nwg, a.err);
-        CQR_STAMP(8);
-        gram_reduce(L, gp2, ewl, nwg, e, false, gfin, wg, a.ctr, 4 * nwg, a.err);
-        CQR_STAMP(9);
-        for (int el = tid; el < 1024; el += kCT) L.tq[el >> 5][el & 31] = q1top[el];
-        __syncthreads();
-        if (w == 0) {
-            // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8
-            // the Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle
-            // of E with half its diagonal) and its inverse I - U1 + O(E^2):
-            // both to working accuracy, without the 32-step factorization.
-            const int c = lane & 31;
+            const int c = lane & 31, i0 = (lane >> 5) * 16;
             double em = 0;
 #pragma unroll
-            for (int i = 0; i < 32; ++i) em = fmax(em, fabs(L.g[i][c] - (i == c ? 1.0 : 0.0)));
-            for (int o = 16; o >= 1; o >>= 1) em = fmax(em, __shfl_xor(em, o, 64));
-            const bool fast = em < 1e-8;   // wave-uniform
-            if (fast) {
-                if (lane < 32) {
+            for (int ii = 0; ii < 16; ++ii) em = fmax(em, fabs(L.g[i0 + ii][c] - (i0 + ii == c ? 1.0 : 0.0)));
+            for (int o = 32; o >= 1; o >>= 1) em = fmax(em, __shfl_xor(em, o, 64));
+            fast = em < 1e-8;   // uniform over the workgroup
+        }
+        if (fast) {
 #pragma unroll
-                    for (int i = 0; i < 32; ++i) {
-                        const double u1 = i < c ? L.g[i][c] : (i == c ? 0.5 * (L.g[c][c] - 1.0) : 0.0);
-                        L.r2[i][c] = (i == c ? 1.0 : 0.0) + u1;
-                        L.r2w[i][c] = i == c ? 1.0 - u1 : u1;   // (reciprocal diagonal, first order)
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // Q_t = Q1_t (I - U1) (lane = row): y[t] = q[t] - sum_{k <= t} q[k] U1[k][t]
-                if (lane < 32) {
-                    typedef double d2 __attribute__((ext_vector_type(2)));
-                    double qv[32], y[32];
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) { qv[t] = L.tq[lane][t]; y[t] = qv[t]; }
-#pragma unroll
-                    for (int k = 0; k < 32; ++k) {
-                        d2 rr[16];
-#pragma unroll
-                        for (int p = k / 2; p < 16; ++p) rr[p] = *(const d2 *)&L.r2[k][2 * p];
-#pragma unroll
-                        for (int t = k; t < 32; ++t) {
-                            const double u = ((t & 1) ? rr[t >> 1].y : rr[t >> 1].x) - (t == k ? 1.0 : 0.0);
-                            y[t] = fma(-qv[k], u, y[t]);
-                        }
-                    }
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) L.tq[lane][t] = y[t];
-                }
-            } else {
-                const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
-                if (lane == 0 && !good) L.flags = 1;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // Q_t = Q1_t R2^-1 (lane = row)
-                if (lane < 32) {
-                    double y[32];
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) y[t] = L.tq[lane][t];
-                    trsm_row(y, L.r2w);
-#pragma unroll
-                    for (int t = 0; t < 32; ++t) L.tq[lane][t] = y[t];
-                }
+            for (int u = 0; u < 4; ++u) {
+                const int el = tid + kCT * u, r = el >> 5, c = el & 31;
+                const double u1 = r < c ? L.g[r][c] : (r == c ? 0.5 * (L.g[c][c] - 1.0) : 0.0);
+                L.r2[r][c] = (r == c ? 1.0 : 0.0) + u1;
+                L.r2w[r][c] = (r == c ? 1.0 : 0.0) - u1;
             }
+        } else if (w == 0) {
+            const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
+            if (lane == 0 && !good) L.flags = 1;
+        }
+        __syncthreads();
+        // Q = Q1 R2^-1, this thread's row
+        {
+            const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
+#pragma unroll
+            for (int p = 0; p < 16; ++p) {
+                const d2v v = q1r[p];
+                x[2 * p] = v.x;
+                x[2 * p + 1] = v.y;
+            }
+        }
+        if (fast) umul_row(x, L.r2w);
+        else      trsm_row(x, L.r2w);
+        if (i >= a.M) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) x[t] = 0.0;
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) x[t] = 0.0;
+    }
+    if (wg == 0 && tid < 32) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) L.tq[tid][t] = x[t];   // Q_t for the LU
+    }
+
+    // ---- V's rows into vdst (and vdst2), zeros into the panel's rows >= 32.
+    // Destinations with unit column stride are written coalesced: the wave's
+    // 64 rows are staged in its LDS tile and each store instruction covers 4
+    // rows x 32 contiguous elements (a lane per row would touch 64 rows per
+    // instruction).  Rows in [rlo, rhi) of this wave only.
+    const int wrow0 = wg * kCT + 64 * w;   // first row of this wave
+    auto store_v = [&](const double (&v)[32], int rlo, int rhi) {
+        typedef typename G2<T>::v2 v2;
+        const bool mine = i >= rlo && i < rhi && i < a.M;
+        if (a.vst == 1 || (vd2 && a.vst2 == 1)) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) L.q[w][lane][t] = v[t];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // modified LU of Q_t - S = L U (lane r = row r; the pivot row is
-            // read back from LDS as 16-byte broadcasts, its owner writes it
-            // after each step)
-            {
-                typedef double d2 __attribute__((ext_vector_type(2)));
-                const int r = lane & 31;
-                double rv[32];
+        }
+        auto rowmajor = [&](T *base, long rs) {
+#pragma unroll 4
+            for (int it = 0; it < 16; ++it) {
+                const int r = 4 * it + (lane >> 4), row = wrow0 + r, cp = 2 * (lane & 15);
+                if (row >= rlo && row < rhi && row < a.M)
+                    *(v2 *)(base + (size_t)row * rs + cp) = v2{(T)L.q[w][r][cp], (T)L.q[w][r][cp + 1]};
+            }
+        };
+        if (a.vst == 1) rowmajor(vd, a.vsi);
+        else if (mine) {
+            T *vr = vd + (size_t)i * a.vsi;
 #pragma unroll
-                for (int cc = 0; cc < 32; ++cc) rv[cc] = L.tq[r][cc];
+            for (int t = 0; t < 32; ++t) vr[t * a.vst] = (T)v[t];
+        }
+        if (vd2) {
+            if (a.vst2 == 1) rowmajor(vd2, a.vsi2);
+            else if (mine) {
+                T *vr2 = vd2 + (size_t)i * a.vsi2;
 #pragma unroll
-                for (int jj = 0; jj < 32; ++jj) {
-                    d2 pr[16];
-#pragma unroll
-                    for (int p = jj / 2; p < 16; ++p) pr[p] = *(const d2 *)&L.tq[jj][2 * p];
-                    double piv = (jj & 1) ? pr[jj >> 1].y : pr[jj >> 1].x;
-                    const double sg = piv >= 0 ? -1.0 : 1.0;
-                    piv -= sg;                                    // |piv| >= 1
-                    double inv = __builtin_amdgcn_rcp(piv);
-                    inv = fma(inv, fma(-piv, inv, 1.0), inv);
-                    inv = fma(inv, fma(-piv, inv, 1.0), inv);
-                    if (r == jj) rv[jj] = piv;
-                    if (r > jj) {
-                        const double l = rv[jj] * inv;
-                        rv[jj] = l;
-#pragma unroll
-                        for (int cc = jj + 1; cc < 32; ++cc) rv[cc] = fma(-l, (cc & 1) ? pr[cc >> 1].y : pr[cc >> 1].x, rv[cc]);
-                    }
-                    if (lane == 0) L.sgn[jj] = sg;
-                    if (jj + 1 < 32) {
-                        if (lane == jj + 1) {
-#pragma unroll
-                            for (int p = (jj + 1) / 2; p < 16; ++p) *(d2 *)&L.tq[jj + 1][2 * p] = d2{rv[2 * p], rv[2 * p + 1]};
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    }
-                }
-                if (lane < 32) {
-#pragma unroll
-                    for (int cc = 0; cc < 32; ++cc) L.u[r][cc] = rv[cc];
-                }
+                for (int t = 0; t < 32; ++t) vr2[t * a.vst2] = (T)v[t];
             }
         }
-        __syncthreads();
-        CQR_STAMP(10);
-        if (L.flags && tid == 0 && wg == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w == 0) {
-            // M = U R2 (lane c = column c): M[i][c] = sum_{k >= i} U[i][k] R2[k][c]
-            const int c = lane & 31;
-            double r2c[32];
-#pragma unroll
-            for (int k = 0; k < 32; ++k) r2c[k] = L.r2[k][c];
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-                double s = 0;
-#pragma unroll
-                for (int k = i; k < 32; ++k) s = fma(L.u[i][k], r2c[k], s);
-                if (lane < 32) L.mm[i][c] = i == c ? 1.0 / s : s;
+    };
+    store_v(x, 32, INT_MAX);
+    {   // zeros below the panel's R block
+        typedef typename G2<T>::v2 v2;
+        if (a.ast == 1) {
+#pragma unroll 4
+            for (int it = 0; it < 16; ++it) {
+                const int row = wrow0 + 4 * it + (lane >> 4), cp = 2 * (lane & 15);
+                if (row >= 32 && row < a.M) *(v2 *)(ap + (size_t)row * a.asi + cp) = v2{(T)0, (T)0};
             }
-        } else if (w == 1 && wg == 0) {
-            // T (lane a = row a): T[a][k] = -U[a][k] s_k - sum_{a <= i < k} L[k][i] T[a][i]
-            const int ar = lane & 31;
-            double tr[32];
-            T *tout = (T *)a.tout;
+        } else if (i >= 32 && i < a.M) {
+            T *arow = ap + (size_t)i * a.asi;
 #pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                double s = ar <= k ? -L.u[ar][k] * L.sgn[k] : 0.0;
-#pragma unroll
-                for (int i = 0; i < k; ++i) s = fma(-L.u[k][i], tr[i], s);   // tr[i] = 0 for i < ar
-                tr[k] = s;
-                if (lane < 32) tout[ar * 32 + k] = (T)s;
-            }
-        } else if (w == 2 && wg == 0) {
-            // R = S R2 R1 2^e (lane c = column c) into the panel
-            const int c = lane & 31;
-            double r1c[32];
-#pragma unroll
-            for (int k = 0; k < 32; ++k) r1c[k] = L.r1[k][c];
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-                double s = 0;
-#pragma unroll
-                for (int k = i; k < 32; ++k) s = fma(L.r2[i][k], r1c[k], s);
-                if (lane < 32) ap[(size_t)i * a.asi + (size_t)c * a.ast] = (T)ldexp(s * L.sgn[i], e);
-            }
+            for (int t = 0; t < 32; ++t) arow[t * a.ast] = (T)0;
         }
-        __syncthreads();
-    } else {
-        // zero panel
-        for (int el = tid; el < 1024; el += kCT) {
-            const int i = el >> 5, t = el & 31;
-            L.u[i][t] = 0;
-            L.mm[i][t] = i == t ? 1.0 : 0.0;
-            if (wg == 0) {
-                ((T *)a.tout)[el] = (T)0;
-                ap[(size_t)i * a.asi + (size_t)t * a.ast] = (T)0;
-            }
-        }
-        __syncthreads();
     }
+    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg != 0) return;
 
-    CQR_STAMP(11);
-    // ---- V = Q1 M^-1 (rows >= 32), L (rows < 32); zeros below R --------------
+    // ---- workgroup 0: the modified LU of Q_t - S, V's top rows, T and R -------
+    lds_barrier();   // L.tq complete (the V stores above need not drain)
+    if (w == 0) {
+        const int r = lane & 31;
+        double rv[32];
 #pragma unroll
-    for (int r = 0; r < kRPT; ++r) {
-        const int i = rowid[r];
-        if (i < 0) continue;
-        T *vr = vd + (size_t)i * a.vsi, *vr2 = vd2 ? vd2 + (size_t)i * a.vsi2 : nullptr;
-        T *arow = ap + (size_t)i * a.asi;
-        const long vst = a.vst, vst2 = a.vst2, ast = a.ast;
-        if (i < 32) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) {
-                const T v = (T)(i > t ? L.u[i][t] : (i == t ? 1.0 : 0.0));
-                vr[t * vst] = v;
-                if (vr2) vr2[t * vst2] = v;
-            }
+        for (int cc = 0; cc < 32; ++cc) rv[cc] = L.tq[r][cc];
+        if (!zero) {
+            lu_wave(rv, L.sgn, lane);
         } else {
-            if (zero) {
 #pragma unroll
-                for (int t = 0; t < 32; ++t) x[r][t] = 0;
-            } else {
-                trsm_row(x[r], L.mm);
-            }
-            typedef typename G2<T>::v2 v2;
-            if (vst == 1) {
+            for (int jj = 0; jj < 32; ++jj) rv[jj] = r == jj ? 1.0 : 0.0;
+            if (lane < 32) L.sgn[lane] = -1.0;
+        }
+        if (lane < 32) {
 #pragma unroll
-                for (int t = 0; t < 32; t += 2) *(v2 *)(vr + t) = v2{(T)x[r][t], (T)x[r][t + 1]};
-            } else {
+            for (int cc = 0; cc < 32; ++cc) L.u[r][cc] = cc >= r ? rv[cc] : 0.0;   // U (upper)
 #pragma unroll
-                for (int t = 0; t < 32; ++t) vr[t * vst] = (T)x[r][t];
-            }
-            if (vr2) {
-                if (vst2 == 1) {
+            for (int cc = 0; cc < 32; ++cc) L.tq[r][cc] = cc < r ? rv[cc] : 0.0;   // L (strict lower)
+        }
+    } else if (w == 3) {
+        for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
+    }
+    lds_barrier();
+    if (w == 0) {
+        // V's top rows: Q_t - S
+        double v[32];
 #pragma unroll
-                    for (int t = 0; t < 32; t += 2) *(v2 *)(vr2 + t) = v2{(T)x[r][t], (T)x[r][t + 1]};
-                } else {
+        for (int t = 0; t < 32; ++t) v[t] = x[t] - (t == lane ? L.sgn[t] : 0.0);
+        store_v(v, 0, 32);
+    } else if (w == 1) {
+        // U^-1 (lane c = column c, right-looking back substitution) -> L.r1w
+        const int c = lane & 31;
+        double acc[32];
 #pragma unroll
-                    for (int t = 0; t < 32; ++t) vr2[t * vst2] = (T)x[r][t];
-                }
-            }
-            if (ast == 1) {
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
 #pragma unroll
-                for (int t = 0; t < 32; t += 2) *(v2 *)(arow + t) = v2{(T)0, (T)0};
-            } else {
+        for (int k = 31; k >= 0; --k) {
+            const double d = L.u[k][k];
+            double inv = __builtin_amdgcn_rcp(d);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            const double xk = acc[k] * inv;
+            acc[k] = xk;
 #pragma unroll
-                for (int t = 0; t < 32; ++t) arow[t * ast] = (T)0;
+            for (int i2 = 0; i2 < k; ++i2) acc[i2] = fma(-L.u[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) L.r1w[k][c] = acc[k];
+        }
+    } else if (w == 2) {
+        // L^-1 (unit lower; lane c = column c, forward substitution) -> L.mm
+        const int c = lane & 31;
+        double acc[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const double xk = acc[k];
+#pragma unroll
+            for (int i2 = k + 1; i2 < 32; ++i2) acc[i2] = fma(-L.tq[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) L.mm[k][c] = acc[k];
+        }
+    } else {
+        // R = S R2 R1 2^e into the panel (matrix cores, four tiles)
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) {
+            const int ti = t4 >> 1, tj = t4 & 1;
+            Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
+            if (tj >= ti && !zero) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
+                ap[(size_t)i2 * a.asi + (size_t)c * a.ast] = (T)(i2 <= c ? ldexp(rt[g] * L.sgn[i2], e) : 0.0);
             }
         }
     }
-
-    // ---- exit: the last workgroup out resets the cluster counters -------------
-    __syncthreads();
-    CQR_STAMP(12);
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(a.ctr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == nwg - 1) {
-            __hip_atomic_store(a.ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lds_barrier();
+    // T = -S (U^-1 L^-1)^T: wave w forms tile (w >> 1, w & 1) of U^-1 L^-1
+    {
+        const int ti = w >> 1, tj = w & 1;
+        const Mf<double>::v4 pt = tile_mm(L.r1w, L.mm, ti, tj, lane, 16 * (ti > tj ? ti : tj), 32);
+        T *tout = (T *)a.tout;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), j2 = 16 * tj + (lane & 15);
+            tout[j2 * 32 + i2] = (T)(zero ? 0.0 : -L.sgn[j2] * pt[g]);
         }
     }
 }
@@ -1371,7 +1393,7 @@ static BlkLayout blk_layout(int m, int n, size_t elem) {
     L.vout = take((size_t)32 * 256 * elem);
     L.qp = take((size_t)32 * L.mp * elem);
     L.tf = take((size_t)8 * 1024 * elem);
-    L.cws = take(cqr_ws_doubles(L.cwg) * sizeof(double));
+    L.cws = take(cqr_ws_doubles() * sizeof(double));
     L.ctr = take(64 * sizeof(int));
     L.total = off;
     return L;
@@ -1379,11 +1401,25 @@ static BlkLayout blk_layout(int m, int n, size_t elem) {
 
 size_t blk_ws_bytes(int m, int n, size_t elem) { return blk_layout(m, n, elem).total; }
 
-int blk_columns(int n, int b) {
-    if (b != 32) return 0;
+int blk_columns(int m, int n, int b) {
+    // panels of up to kCW x 256 rows (the panel QR's workgroup count)
+    if (b != 32 || m > kCW * kCT || n > kCW * kCT) return 0;
     int k0 = 0;
     while (n - k0 >= (NBMAX + 1) * 32) k0 += NBMAX * 32;
     return k0;
+}
+
+// Every launch of the blocked path goes through here: with brd_profile on,
+// the launch itself stamps its start and end (hipExtLaunchKernel), tagged with
+// the kernel's algorithmic flops and HBM bytes (bench.py's roofline objects).
+template <typename F, typename... Args>
+static void blk_launch(const char *kind, double flops, double bytes, F kernel, dim3 grid, dim3 block, hipStream_t s,
+                       Args... args) {
+    hipEvent_t ea, eb;
+    if (api_prof_launch_events(kind, flops, bytes, &ea, &eb))
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ea, eb, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
 }
 
 template <typename T>
@@ -1409,15 +1445,15 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.err = err;
     *ksplit_out = ks;
     dim3 grid(a.nvirt + a.mtiles * ks), block(kRT);
-    if (yp) hipLaunchKernelGGL((k_rpass<T, true>), grid, block, 0, s, a);
-    else    hipLaunchKernelGGL((k_rpass<T, false>), grid, block, 0, s, a);
+    // algorithmic: the K x M source read once, 2 x 32 flops per element
+    const double fl = 2.0 * 32 * K * M, by = (double)K * M * sizeof(T);
+    if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true>, grid, block, s, a);
+    else    blk_launch("s1_rpass", fl, by, k_rpass<T, false>, grid, block, s, a);
+    if (a.nvirt > 0)
+        blk_launch("s1_prep", 0.0, 0.0, k_vsum<T>, dim3(32 * kMT / 256), dim3(256), s, (const T *)a.vpart, (T *)a.vout,
+                   a.nvirt);
     return hipGetLastError();
 }
-
-// BRD_S1_STAMPS=1 (diagnostics): phase clocks of workgroup 0 of every k_cqr
-// launch, averaged and printed to stderr at the end of blk_ge2band.
-static unsigned long long *g_cqr_stamps = nullptr;
-static int g_cqr_calls = 0;
 
 template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
@@ -1428,38 +1464,29 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
     a.vdst2 = vdst2; a.vsi2 = vsi2; a.vst2 = vst2;
     a.tout = tout; a.apan = apan; a.asi = asi; a.ast = ast;
-    int rpt = 1;
-    int nwg = (M + kCT * rpt - 1) / (kCT * rpt);
+    const int nwg = (M + kCT - 1) / kCT;
     if (nwg > Ly.cwg) return hipErrorInvalidValue;
-    a.rpt = rpt;
     a.ws = (double *)(ws + Ly.cws);
-    a.ctr = (int *)(ws + Ly.ctr);
     a.err = err;
-    a.stamps = g_cqr_stamps ? g_cqr_stamps + 16 * g_cqr_calls : nullptr;
-    if (g_cqr_stamps && g_cqr_calls < 1023) ++g_cqr_calls;
-    hipLaunchKernelGGL((k_cqr<T>), dim3(nwg), dim3(kCT), 0, s, a);
+    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a);
+    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a);
+    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T>, dim3(nwg), dim3(kCT), s, a);
     return hipGetLastError();
 }
 
-// Blocked stage 1 over columns [0, kend) (kend = blk_columns(n, 32) > 0);
+// Blocked stage 1 over columns [0, kend) (kend = blk_columns(m, n, 32) > 0);
 // the caller finishes the remaining panels with the per-panel path.
 template <typename T>
 hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, int target, int *err) {
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, n, sizeof(T));
-    const int kend = blk_columns(n, 32);
+    const int kend = blk_columns(m, n, 32);
     T *Lw = (T *)(ws + Ly.lw), *RwT = (T *)(ws + Ly.rwt), *Ub = (T *)(ws + Ly.ub);
     T *tf = (T *)(ws + Ly.tf);   // T_j at tf + 1024 j, S_j at tf + 1024 (4 + j)
     int *ctr = (int *)(ws + Ly.ctr);
     const long ldr = Ly.ldr;
-    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);   // cluster / last-arriver counters
+    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);   // the read passes' last-arriver counters
     if (e != hipSuccess) return e;
-    const char *stenv = getenv("BRD_S1_STAMPS");
-    if (stenv && stenv[0] == '1') {
-        if (!g_cqr_stamps) hipMalloc(&g_cqr_stamps, 1024 * 16 * sizeof(unsigned long long));
-        hipMemsetAsync(g_cqr_stamps, 0, 1024 * 16 * sizeof(unsigned long long), s);
-        g_cqr_calls = 0;
-    }
     int ks_x = 1;
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
@@ -1478,7 +1505,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.G = ws + Ly.vout; p.Tm = tf + 1024 * (NBMAX + j - 1);
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
-                hipLaunchKernelGGL((k_prep_qr<T>), dim3((mr + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+                blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((mr + kPI - 1) / kPI), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 32, 1, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -1497,7 +1524,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.G = ws + Ly.vout; p.Tm = Tj;
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
-                hipLaunchKernelGGL((k_prep_lq<T>), dim3((n2 + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+                blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, dim3((n2 + kPI - 1) / kPI), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -1519,7 +1546,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.G = ws + Ly.vout; p.Tm = tf + 1024 * (2 * NBMAX - 1);
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
-            hipLaunchKernelGGL((k_prep_qr<T>), dim3((m - k1 + kPI - 1) / kPI), dim3(kPT), 0, s, p);
+            blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((m - k1 + kPI - 1) / kPI), dim3(kPT), s, p);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -1531,31 +1558,13 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             g.K = 256;
             g.tiles_c = (g.cols + kGM - 1) / kGM;
             const int tiles_r = (g.rows + kGM - 1) / kGM;
-            hipLaunchKernelGGL((k_blkupd<T>), dim3(tiles_r * g.tiles_c), dim3(kGT), 0, s, g);
+            // algorithmic: C read and written once, Lw / RwT read once; 2 x 256 flops per element
+            const double el = (double)g.rows * g.cols;
+            blk_launch("s1_blkupd", 2.0 * 256 * el, (2.0 * el + 256.0 * (g.rows + g.cols)) * sizeof(T), k_blkupd<T>,
+                       dim3(tiles_r * g.tiles_c), dim3(kGT), s, g);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-    }
-    if (stenv && stenv[0] == '1' && g_cqr_stamps) {
-        std::vector<unsigned long long> h(1024 * 16);
-        hipStreamSynchronize(s);
-        hipMemcpy(h.data(), g_cqr_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-        double acc[16] = {0};
-        int cnt = 0;
-        for (int i = 0; i < g_cqr_calls; ++i) {
-            const unsigned long long *st = &h[16 * i];
-            if (!st[0] || !st[12]) continue;
-            ++cnt;
-            unsigned long long prev = st[0];
-            for (int k = 1; k <= 12; ++k) {
-                if (!st[k]) continue;
-                acc[k] += (double)(st[k] - prev);
-                prev = st[k];
-            }
-        }
-        fprintf(stderr, "k_cqr phases (clocks, mean over %d launches):", cnt);
-        for (int k = 1; k <= 12; ++k) fprintf(stderr, " %d:%.0f", k, cnt ? acc[k] / cnt : 0.0);
-        fprintf(stderr, "\n");
     }
     return hipSuccess;
 }

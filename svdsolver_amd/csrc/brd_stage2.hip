@@ -465,26 +465,41 @@ __device__ __forceinline__ T group_sum(T v) {
     return v;
 }
 // 1/sqrt(q) and 1/u: hardware estimate refined by Newton steps to full precision
+// The hardware estimates flush denormal inputs and results, so arguments
+// near the ends of the exponent range are rescaled by a power of two first
+// (exact): a squared norm below 2^-960 (fp64) / 2^-100 (fp32), a reciprocal
+// argument outside 2^+-960 / 2^+-100.
 __device__ __forceinline__ double rsq_nr(double q) {
-    double r = __builtin_amdgcn_rsq(q);
-    const double h = 0.5 * q;
+    const bool tiny = q < 0x1p-960;
+    const double qs = tiny ? q * 0x1p+1000 : q;
+    double r = __builtin_amdgcn_rsq(qs);
+    const double h = 0.5 * qs;
     r = r * fma(-h * r, r, 1.5);
     r = r * fma(-h * r, r, 1.5);
-    return r;
+    return tiny ? r * 0x1p+500 : r;
 }
 __device__ __forceinline__ float rsq_nr(float q) {
-    float r = __builtin_amdgcn_rsqf(q);
-    return r * fmaf(-0.5f * q * r, r, 1.5f);
+    const bool tiny = q < 0x1p-100f;
+    const float qs = tiny ? q * 0x1p+100f : q;
+    const float r = __builtin_amdgcn_rsqf(qs);
+    const float rr = r * fmaf(-0.5f * qs * r, r, 1.5f);
+    return tiny ? rr * 0x1p+50f : rr;
 }
 __device__ __forceinline__ double rcp_nr(double u) {
-    double y = __builtin_amdgcn_rcp(u);
-    y = fma(y, fma(-u, y, 1.0), y);
-    y = fma(y, fma(-u, y, 1.0), y);
-    return y;
+    const double au = fabs(u);
+    const double sc = au < 0x1p-960 ? 0x1p+960 : (au > 0x1p+960 ? 0x1p-960 : 1.0);
+    const double us = u * sc;
+    double y = __builtin_amdgcn_rcp(us);
+    y = fma(y, fma(-us, y, 1.0), y);
+    y = fma(y, fma(-us, y, 1.0), y);
+    return y * sc;
 }
 __device__ __forceinline__ float rcp_nr(float u) {
-    const float y = __builtin_amdgcn_rcpf(u);
-    return fmaf(y, fmaf(-u, y, 1.0f), y);
+    const float au = fabsf(u);
+    const float sc = au < 0x1p-100f ? 0x1p+100f : (au > 0x1p+100f ? 0x1p-100f : 1.0f);
+    const float us = u * sc;
+    const float y = __builtin_amdgcn_rcpf(us);
+    return fmaf(y, fmaf(-us, y, 1.0f), y) * sc;
 }
 // Apply the reflector of the source vector x (x0 = its element 0, the pivot)
 // to a; this lane holds elements [q E, q E + E) of both.

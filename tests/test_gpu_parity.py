@@ -433,3 +433,33 @@ def test_padded_leading_dimension(S):
     sv_ref = np.linalg.svd(A, compute_uv=False)
     assert np.max(np.abs(_sv_bidiag(d.cpu().numpy(), e.cpu().numpy()) - sv_ref)) / sv_ref[0] < 1e-12
     assert torch.all(P[:, n:] == 7.0)
+
+
+# ---- blocked stage 1 (brd_stage1_blk.hip) against the per-panel kernels ----
+@pytest.mark.parametrize("m,n,T", [(1024, 1024, "double"), (2048, 2048, "double"), (1500, 1024, "double"),
+                                   (1024, 1024, "float")])
+def test_blocked_stage1_matches_per_panel(S, m, n, T):
+    """The blocked stage 1 (the default for b = 32: delayed two-sided update,
+    CholeskyQR2 panels in basis-kernel form) and the per-panel tree kernels
+    (BRD_S1_BLOCKED=0) give the same band up to signs: |band| normwise fp64
+    <= 1e-13, fp32 <= 5e-5; both with exact zeros outside the band."""
+    import os
+    rng = np.random.default_rng(m + n)
+    A = (rng.random((m, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get("BRD_S1_BLOCKED")
+    try:
+        os.environ["BRD_S1_BLOCKED"] = "0"
+        B0 = S.brd_p1(A, 32)
+        os.environ["BRD_S1_BLOCKED"] = "1"
+        B1 = S.brd_p1(A, 32)
+    finally:
+        if old is None:
+            os.environ.pop("BRD_S1_BLOCKED", None)
+        else:
+            os.environ["BRD_S1_BLOCKED"] = old
+    i, j = np.indices((m, n))
+    msk = (j >= i) & (j - i <= 32)
+    assert np.all(B1[~msk] == 0) and np.all(B0[~msk] == 0)
+    d = np.linalg.norm(np.abs(B1[msk].astype(np.float64)) - np.abs(B0[msk].astype(np.float64)))
+    d /= np.linalg.norm(B0[msk].astype(np.float64))
+    assert d <= (1e-13 if T == "double" else 5e-5), d

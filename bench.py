@@ -211,7 +211,7 @@ def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):
                 continue
             tot += d * (two_fetch + wr) * 1024 * 1024
             cnt += d
-    return (tot / cnt if cnt else None), os.path.relpath(files[-1], REPO)
+    return (tot / cnt, os.path.relpath(files[-1], REPO)) if cnt else (None, None)
 
 
 def apply_roofline(ap, dtype, n):
@@ -416,6 +416,11 @@ def main():
     s2_cus = S.overlap_cus(n) if pipelined else 0
     if args.s2_cus is not None:
         s2_cus = args.s2_cus
+    lanes = args.lanes if pipelined else 1
+    if pipelined and lanes * max(s2_cus, 1) > torch.cuda.get_device_properties(dev).multi_processor_count:
+        # every lane's stage-2 kernel is a persistent grid of s2_cus workgroups,
+        # one per CU: together they must fit the chip
+        sys.exit(f"bench.py: lanes * s2_cus = {lanes} * {s2_cus} exceeds the device's CUs")
     S.set_overlap(s2_cus)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -435,7 +440,6 @@ def main():
     # world size 1 over RCCL (--force-dist, 12 steps), 14.6 vs 16.0 -- across
     # GPUs a matrix's stage 1 is a chain of per-panel collectives and factors,
     # so more matrices in flight hide more of it.
-    lanes = args.lanes if pipelined else 1
     sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
     sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
     if dist_mode:

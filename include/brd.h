@@ -105,6 +105,14 @@ int brd_set_overlap(int s2_cus);   /* 0 <= s2_cus < device CUs, else BRD_EINVAL 
  * asynchronous work before trusting the results. */
 int brd_check_errors(void);
 
+/* Drain hip_stream (NULL: the library's current stream) and free the
+ * library's per-stream state for it: stage-1/stage-2 workspaces, the cached
+ * HBM staging buffer of host-pointer calls, the stage-2 error word (read
+ * first: BRD_EHIP if it was set).  brd_check_errors() visits every stream the
+ * library has launched on, so call this before destroying such a stream.
+ * Host-pointer calls free a staging buffer above 256 MiB on return. */
+int brd_release_stream(void *hip_stream);
+
 /* Per-kernel device timing for roofline reporting.  While enabled, the library
  * brackets every launch of the named kernel class with HIP events on the
  * launch stream.  kernel: "s1_apply", "s1_factor", "s2_sweep".  Returns the

@@ -37,7 +37,7 @@ BRD_SIGMA = 0x10
 
 EXPORTED = (
     "brd_ge2band_f64", "brd_ge2band_f32", "brd_band2bd_f64", "brd_band2bd_f32",
-    "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_check_errors", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
+    "brd_set_stream", "brd_use_own_stream", "brd_set_overlap", "brd_check_errors", "brd_release_stream", "brd_profile_enable", "brd_profile_reset", "brd_profile_query",
     "brd_dist_unique_id", "brd_dist_init", "brd_dist_init_host", "brd_dist_finalize", "brd_dist_local_cols",
     "brd_ge2band_dist_f64", "brd_ge2band_dist_f32", "brd_dist_gather_band_f64", "brd_dist_gather_band_f32",
     "brd_bdsvd_f64", "brd_bdsvd_f32", "brd_bdsvd_dev_f64", "brd_bdsvd_dev_f32", "brd_last_error", "brd_version",
@@ -94,6 +94,8 @@ def _load() -> ctypes.CDLL:
     L.brd_set_overlap.restype = ci
     L.brd_check_errors.argtypes = []
     L.brd_check_errors.restype = ci
+    L.brd_release_stream.argtypes = [ctypes.c_void_p]
+    L.brd_release_stream.restype = ci
     L.brd_profile_enable.argtypes = [ci]
     L.brd_profile_enable.restype = ci
     L.brd_profile_reset.argtypes = []
@@ -344,6 +346,14 @@ def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = No
     dev = mats[0].device
     cus = overlap_cus(mats[0].shape[0]) if s2_cus is None else int(s2_cus)
     lanes = min(int(lanes), len(mats))
+    # every lane's stage-2 kernel is a persistent grid of ``cus`` workgroups,
+    # one per CU (its LDS ring takes the CU), whose bundles wait on each
+    # other: with more workgroups in flight than the chip holds, a partly
+    # resident grid stalls ("Overlap and lanes")
+    dev_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    if lanes * cus > dev_cus:
+        raise ValueError(f"lanes * s2_cus = {lanes} * {cus} exceeds the device's {dev_cus} CUs "
+                         "(stage-2 grids must fit the chip together)")
     s_a = [torch.cuda.Stream(dev) for _ in range(lanes)]
     s_b = [torch.cuda.Stream(dev) for _ in range(lanes)]
     for s in s_a:
@@ -368,6 +378,15 @@ def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = No
         torch.cuda.synchronize(dev)
         check_errors()
     return out
+
+
+def release_stream(stream=None) -> None:
+    """brd_release_stream (include/brd.h): drain ``stream`` (a torch CUDA
+    stream; None: the library's current stream) and free the library's
+    per-stream workspaces, staging buffer and error word; call before the
+    stream is destroyed."""
+    h = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    _check("brd_release_stream", lib.brd_release_stream(h))
 
 
 def check_errors() -> None:

@@ -39,7 +39,6 @@ static int fail(int code, const char *fmt, ...) {
 static const char *err_word_text(int code) {
     switch (code) {
         case 1: return "stage-2 pipeline stalled (spin limit hit)";
-        case 2: return "stage-1 panel cluster barrier timed out";
         case 3: return "stage-1 CholeskyQR panel breakdown";
         default: return "device error";
     }
@@ -227,6 +226,19 @@ static int ensure_stage(size_t bytes, void **out) {
     }
     *out = w.stage;
     return BRD_OK;
+}
+
+// Host-pointer calls stage the matrix in HBM; a staging buffer above this
+// size is freed when the call returns instead of being kept for the stream's
+// lifetime (2 GiB at 16384^2 fp64).
+static const size_t kStageKeep = (size_t)256 << 20;
+static void trim_stage(Ctx::Slot &w) {
+    if (w.stage && w.stage_bytes > kStageKeep) {
+        hipStreamSynchronize(w.s);
+        hipFree(w.stage);
+        w.stage = nullptr;
+        w.stage_bytes = 0;
+    }
 }
 
 static int device_cus() {
@@ -546,6 +558,7 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
             HIP_TRY(hipMemcpy2DAsync(A, sizeof(T) * lda, d, sizeof(T) * n, sizeof(T) * n, m,
                                      hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        trim_stage(slot());
     }
     if (rc == BRD_OK) {
         hipError_t e = hipGetLastError();
@@ -604,6 +617,7 @@ static int band2bd(T *A, int n, int lda, int b, T *dd, T *ee, unsigned flags) {
             HIP_TRY(hipMemcpyAsync(ee, de + n, sizeof(T) * (n - 1), hipMemcpyDeviceToHost, s));
         }
         HIP_TRY(hipStreamSynchronize(s));
+        trim_stage(slot());
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(BRD_EHIP, "stage 2: %s", hipGetErrorString(e));
@@ -685,8 +699,31 @@ int brd_check_errors(void) {
     if (e != hipSuccess) return brd::fail(BRD_EHIP, "HIP error: %s", hipGetErrorString(e));
     if (!bad.empty())
         return brd::fail(BRD_EHIP, "device error word set in an asynchronous call (1: stage-2 spin limit, "
-                                    "2: stage-1 cluster barrier, 3: stage-1 panel breakdown; codes %s)", bad.c_str());
+                                    "3: stage-1 panel breakdown; codes %s)", bad.c_str());
     return BRD_OK;
+}
+
+int brd_release_stream(void *hip_stream) {
+    std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
+    const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : brd::stream();
+    auto &slots = brd::g_ctx.slots;
+    for (auto it = slots.begin(); it != slots.end(); ++it) {
+        if (it->s != s) continue;
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return brd::fail(BRD_EHIP, "brd_release_stream: %s", hipGetErrorString(e));
+        int code = 0;
+        int h = 0;
+        if (it->s2_err && hipMemcpy(&h, it->s2_err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) code = h;
+        if (it->ws) hipFree(it->ws);
+        if (it->s2_flags) hipFree(it->s2_flags);
+        if (it->s2_err) hipFree(it->s2_err);
+        if (it->stage) hipFree(it->stage);
+        slots.erase(it);
+        if (code)
+            return brd::fail(BRD_EHIP, "brd_release_stream: the stream's device error word was set (code %d)", code);
+        return BRD_OK;
+    }
+    return BRD_OK;   // the library never launched on it
 }
 
 int brd_use_own_stream(void) {

@@ -81,6 +81,14 @@ int bdsvd(const T *d_in, const T *e_in, int n, T *sv) {
             return brd::api_fail(BRD_EINVAL, "d / e hold a non-finite value");
         bnorm = std::max(bnorm, std::fabs(d[i]) + (i + 1 < n ? std::fabs(e[i]) : (T)0));
     }
+    // scale to bnorm ~ 1 by a power of two (exact): the shifts and rotations
+    // square their arguments, which would leave the exponent range for
+    // entries near its ends (LAPACK's dbdsqr scales the same way)
+    int ex = 0;
+    if (bnorm > (T)0) std::frexp(bnorm, &ex);
+    for (int i = 0; i < n; ++i) d[i] = std::ldexp(d[i], -ex);
+    for (int i = 0; i + 1 < n; ++i) e[i] = std::ldexp(e[i], -ex);
+    bnorm = std::ldexp(bnorm, -ex);
     const T tiny = eps * bnorm;
     long iters = 0;
     const long max_iters = 30L * n + 100;
@@ -130,7 +138,7 @@ int bdsvd(const T *d_in, const T *e_in, int n, T *sv) {
         }
         gk_step(d.data() + p, e.data() + p, q - p);
     }
-    for (int i = 0; i < n; ++i) sv[i] = std::fabs(d[i]);
+    for (int i = 0; i < n; ++i) sv[i] = std::ldexp(std::fabs(d[i]), ex);
     std::sort(sv, sv + n, std::greater<T>());
     return BRD_OK;
 }

@@ -650,9 +650,11 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 // (Q' is orthogonal and Q' [S; 0] = Q for any sign matrix S with W_t = Q_t - S
 // invertible -- the basis-kernel representation of Sun and Bischof; the
 // modified LU's sign choice keeps W_t well conditioned, as in the Householder
-// reconstruction.)  All arithmetic in fp64.  A Cholesky pivot that is not
-// positive or below 1e-7 x the largest (panel condition number beyond ~1e7,
-// where CholeskyQR2 loses orthogonality) sets the error word (3).
+// reconstruction.)  All arithmetic in fp64.  A first-pass Cholesky pivot
+// that is not positive or below 1e-7 x the largest (panel condition number
+// beyond ~1e7, where CholeskyQR2 loses orthogonality) switches the panel to
+// shifted CholeskyQR3 (k_cqr_q1's shift, k_cqr_q2's extra pass); a breakdown
+// after that sets the error word (3).
 // ==========================================================================
 constexpr int kCT = 256;
 constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
@@ -669,16 +671,16 @@ struct CqrArgs {
     int *err;
 };
 
-// scratch (doubles): the two Gram passes' partials [kCW][1024] each, the
-// per-workgroup exponents, R1, and Q1's rows [kCW kCT][32]
+// scratch (doubles): the three Gram passes' partials [kCW][1024] each, the
+// per-workgroup exponents, R1, the shifted-pass flag, and Q1's rows [kCW kCT][32]
 __host__ __device__ constexpr size_t cqr_ws_doubles() {
-    return (size_t)2 * 1024 * kCW + kCW + 1024 + (size_t)kCW * kCT * 32;
+    return (size_t)3 * 1024 * kCW + kCW + 1024 + 2 + (size_t)kCW * kCT * 32;
 }
 struct CqrWs {
-    double *gp1, *gp2, *ew, *r1, *q1;
+    double *gp1, *gp2, *gp3, *ew, *r1, *shifted, *q1;
     __device__ explicit CqrWs(double *ws)
-        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 2048 * kCW), r1(ws + 2048 * kCW + kCW),
-          q1(ws + 2048 * kCW + kCW + 1024) {}
+        : gp1(ws), gp2(ws + 1024 * kCW), gp3(ws + 2048 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
+          shifted(ws + 3072 * kCW + kCW + 1024), q1(ws + 3072 * kCW + kCW + 1024 + 2) {}
 };
 
 struct CqrLds {
@@ -995,18 +997,35 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     const int i = wg * kCT + tid;
     double x[32];
     if (e == INT_MIN) {   // zero panel: k_cqr_v writes V = [I; 0], T = 0, R = 0
+        if (wg == 0 && tid == 0) W.shifted[0] = 0.0;
         return;
     }
     gram_sum_all(L, W.gp1, L.scl, nwg);
     __syncthreads();
     if (w == 0) {
-        const bool good = chol_wave(L.g, L.r1, L.r1w, lane);
-        if (lane == 0 && !good) L.flags = 1;
+        bool good = chol_wave(L.g, L.r1, L.r1w, lane);
+        if (!good) {
+            // an ill-conditioned panel (cond > ~1e7, e.g. numerically rank
+            // deficient): the shifted Cholesky of sCQR3 (Fukaya et al. 2020),
+            // G + s I with s = 11 (32 M + 32 33) u tr(G); then Q1 has
+            // cond ~ 1e3 and k_cqr_q2 re-orthogonalises it once more
+            double tr = 0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) tr += L.g[k][k];
+            const double sh = 11.0 * (32.0 * a.M + 32.0 * 33.0) * 0x1p-53 * tr;
+            if (lane < 32) L.g[lane][lane] += sh;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            good = chol_wave(L.g, L.r1, L.r1w, lane);
+            if (lane == 0) L.flags = good ? 2 : 1;
+        }
     }
     __syncthreads();
-    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (L.flags == 1 && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wg == 0) {
         for (int el = tid; el < 1024; el += kCT) W.r1[el] = L.r1[el >> 5][el & 31];
+        if (tid == 0) W.shifted[0] = L.flags == 2 ? 1.0 : 0.0;
     }
     // Q1 = (P 2^-e) R1^-1
     cqr_load_row<T>(a, i, x);
@@ -1025,6 +1044,56 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
 }
 
+// After a shifted first pass only (W.shifted; every workgroup returns at once
+// otherwise): one more CholeskyQR pass on Q1 -- Q1 <- Q1 R^-1, R1 <- R R1 --
+// and the Gram partial of the new Q1 into gp3 (sCQR3's middle pass).
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a) {
+    __shared__ CqrLds L;
+    CqrWs W(a.ws);
+    if (W.shifted[0] == 0.0) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
+    if (tid == 0) L.flags = 0;
+    cqr_exponent(L, W.ew, nwg, true);
+    gram_sum_all(L, W.gp2, L.scl, nwg);
+    __syncthreads();
+    if (w == 0) {
+        const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
+        if (lane == 0 && !good) L.flags = 1;
+    }
+    __syncthreads();
+    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int i = wg * kCT + tid;
+    double x[32];
+    d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+        const d2v v = q1r[p];
+        x[2 * p] = v.x;
+        x[2 * p + 1] = v.y;
+    }
+    trsm_row(x, L.r2w);
+    if (i >= a.M) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) x[t] = 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
+    if (wg == 0) {   // R1 <- R R1 (waves 0-3: one tile each)
+        for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
+        __syncthreads();
+        const int ti = w >> 1, tj = w & 1;
+        Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
+        if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
+            W.r1[i2 * 32 + c] = i2 <= c ? rt[g] : 0.0;
+        }
+    }
+    cqr_gram_partial(L, x, W.gp3 + (size_t)wg * 1024);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr_v(CqrArgs a) {
     __shared__ CqrLds L;
@@ -1039,7 +1108,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     T *vd2 = (T *)a.vdst2;
     double x[32];
     if (!zero) {
-        gram_sum_all(L, W.gp2, L.scl, nwg);
+        gram_sum_all(L, W.shifted[0] != 0.0 ? W.gp3 : W.gp2, L.scl, nwg);
         __syncthreads();
         // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
         // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
@@ -1470,6 +1539,7 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.err = err;
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a);
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a);
+    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q2<T>, dim3(nwg), dim3(kCT), s, a);   // returns at once unless shifted
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T>, dim3(nwg), dim3(kCT), s, a);
     return hipGetLastError();
 }

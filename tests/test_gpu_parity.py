@@ -463,3 +463,24 @@ def test_blocked_stage1_matches_per_panel(S, m, n, T):
     d = np.linalg.norm(np.abs(B1[msk].astype(np.float64)) - np.abs(B0[msk].astype(np.float64)))
     d /= np.linalg.norm(B0[msk].astype(np.float64))
     assert d <= (1e-13 if T == "double" else 5e-5), d
+
+
+def test_release_stream_frees_and_keeps_working(S):
+    """brd_release_stream: a stream the library launched on can be released
+    (drained, its workspaces and error word freed) and destroyed; a later
+    brd_check_errors does not touch it, and the library keeps working on new
+    streams."""
+    import torch
+    A = torch.rand(512, 512, dtype=torch.float64, device="cuda") * 5
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        M = A.clone()
+        S.ge2band(M, 32, sync=False)
+        band = M.clone()
+        d, e = S.band2bd(M, 32, sync=False)
+    S.release_stream(st)
+    del st
+    S.check_errors()
+    M2 = A.clone()
+    S.ge2band(M2, 32)
+    assert torch.equal(band, M2)

@@ -99,17 +99,26 @@ struct RpArgs {
     void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
     void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
     void *vout;                     // virtual result [32][256] / [256][32]
-    int *counter;                   // virtual workgroups finished (0 between launches)
+    int *counter;                   // (unused)
     int *err;
+    int has_fin;                    // 1: workgroup 0 runs cqr_finish of the panel the pass follows
 };
 
-template <typename T, bool YP>
-__global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a) {
+struct FinArgs;
+template <typename T>
+__device__ void cqr_finish_entry(const FinArgs &f, int tid);
+
+template <typename T, bool YP, typename FA>
+__global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a, FA fin) {
     typedef typename G2<T>::v2 v2;
     typedef typename Mf<T>::v4 v4;
     const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, kh = tid >> 8;
     const int q = lane >> 4, l15 = lane & 15;
-    const int bid = blockIdx.x;
+    if (a.has_fin && blockIdx.x == 0) {   // the previous panel's LU, T and R signs, beside the pass
+        cqr_finish_entry<T>(fin, tid);
+        return;
+    }
+    const int bid = blockIdx.x - a.has_fin;
     const bool virt = bid < a.nvirt;
     int mx, ks;
     if (virt) { mx = 0; ks = bid; }
@@ -257,9 +266,14 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a) {
 // The virtual tile's split-K partials summed in fixed order (one element per
 // thread, every partial's load in flight at once): a kernel of its own, so
 // no workgroup of the read pass waits for another.
+// Workgroup 0 also patches the diagonal of the finished panel's top block
+// from V' = Q to V = Q - S (pbase[t (pstride)] -= s_t), read from here on.
 template <typename T>
-__global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt) {
+__global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt, T *pbase, long pstride,
+                                              const double *sgn) {
     const int e = blockIdx.x * 256 + threadIdx.x;   // < 32 kMT
+    if (blockIdx.x == 0 && threadIdx.x < 32 && pbase)
+        pbase[(size_t)threadIdx.x * pstride] = (T)((double)pbase[(size_t)threadIdx.x * pstride] - sgn[threadIdx.x]);
     T v[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) v[k] = vpart[(size_t)min(k, nvirt - 1) * 32 * kMT + e];
@@ -304,6 +318,7 @@ struct PrepArgs {
     int j;                    // panel index in the block
     int items;
     int reduce, factor;       // QR side switches
+    const double *sgn;        // s_t of the panel whose pass preceded (V' = Q was used: corrections)
 };
 
 constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
@@ -422,10 +437,15 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
                 for (int g = 0; g < 4; ++g)
                     if (k0 + u < a.ksplit) y[h][g] += v[u][h][g];
     }
+    // the pass used V' = Q (top rows without -S): A_cur^T V = A_cur^T V' -
+    // A_cur[c:c+32, :]^T S, and aq here is exactly A_cur[c+t][col]
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) y[h][g] = iv ? y[h][g] - ay[h][g] : (T)0;
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            y[h][g] = iv ? y[h][g] - ay[h][g] - (T)a.sgn[t] * aq[h][g] : (T)0;
+        }
     // ---- Y_j^T = T_j^T y^T: the C registers of y are the B operand -----------
     v4 ayj[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
 #pragma unroll
@@ -582,7 +602,10 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int r = Mf<T>::crow(q, g), t = 16 * h + l15;
-            Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] : (T)0;
+            // the pass used U' = Q: ap here is A_cur[row][c + t] (corrections;
+            // the block end's reduce-only call follows an inline finish: none)
+            const T corr = a.factor ? (T)a.sgn[t] * ap[h][g] : (T)0;
+            Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] - corr : (T)0;
         }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -674,13 +697,18 @@ struct CqrArgs {
 // scratch (doubles): the three Gram passes' partials [kCW][1024] each, the
 // per-workgroup exponents, R1, the shifted-pass flag, and Q1's rows [kCW kCT][32]
 __host__ __device__ constexpr size_t cqr_ws_doubles() {
-    return (size_t)3 * 1024 * kCW + kCW + 1024 + 2 + (size_t)kCW * kCT * 32;
+    return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
 }
+// Q_t (qt) and the zero flag are read by the next read pass's finishing
+// workgroup (cqr_finish)
+__host__ __device__ constexpr size_t cqr_ws_qt() { return (size_t)3 * 1024 * kCW + kCW + 1024; }
+__host__ __device__ constexpr size_t cqr_ws_zero() { return cqr_ws_qt() + 1024 + 2; }
 struct CqrWs {
-    double *gp1, *gp2, *gp3, *ew, *r1, *shifted, *q1;
+    double *gp1, *gp2, *gp3, *ew, *r1, *qt, *shifted, *zero, *q1;
     __device__ explicit CqrWs(double *ws)
         : gp1(ws), gp2(ws + 1024 * kCW), gp3(ws + 2048 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
-          shifted(ws + 3072 * kCW + kCW + 1024), q1(ws + 3072 * kCW + kCW + 1024 + 2) {}
+          qt(ws + cqr_ws_qt()), shifted(ws + cqr_ws_qt() + 1024), zero(ws + cqr_ws_zero()),
+          q1(ws + cqr_ws_zero() + 2) {}
 };
 
 struct CqrLds {
@@ -1044,15 +1072,17 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
 }
 
-// After a shifted first pass only (W.shifted; every workgroup returns at once
-// otherwise): one more CholeskyQR pass on Q1 -- Q1 <- Q1 R^-1, R1 <- R R1 --
-// and the Gram partial of the new Q1 into gp3 (sCQR3's middle pass).
+// After a shifted first pass only (W.shifted; it returns at once otherwise):
+// one more CholeskyQR pass on Q1 -- Q1 <- Q1 R^-1, R1 <- R R1 -- and the
+// Gram of the new Q1 into gp3 (sCQR3's middle pass).  ONE workgroup walks all
+// rows (the rare ill-conditioned panel pays ~0.1-0.2 ms; the common case pays
+// only a one-workgroup launch instead of a panel-wide one).
 template <typename T>
-__global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a) {
+__global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a, int nwg) {
     __shared__ CqrLds L;
     CqrWs W(a.ws);
     if (W.shifted[0] == 0.0) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) L.flags = 0;
     cqr_exponent(L, W.ew, nwg, true);
     gram_sum_all(L, W.gp2, L.scl, nwg);
@@ -1063,25 +1093,30 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a) {
     }
     __syncthreads();
     if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int i = wg * kCT + tid;
-    double x[32];
-    d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
+    double gacc[3][4] = {};
+    for (int chunk = 0; chunk < nwg; ++chunk) {
+        const int i = chunk * kCT + tid;
+        double x[32];
+        d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
 #pragma unroll
-    for (int p = 0; p < 16; ++p) {
-        const d2v v = q1r[p];
-        x[2 * p] = v.x;
-        x[2 * p + 1] = v.y;
+        for (int p = 0; p < 16; ++p) {
+            const d2v v = q1r[p];
+            x[2 * p] = v.x;
+            x[2 * p + 1] = v.y;
+        }
+        trsm_row(x, L.r2w);
+        if (i >= a.M) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) x[t] = 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
+        gram_wave(L, w, lane, x, gacc);
     }
-    trsm_row(x, L.r2w);
-    if (i >= a.M) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = 0.0;
-    }
-#pragma unroll
-    for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
-    if (wg == 0) {   // R1 <- R R1 (waves 0-3: one tile each)
-        for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
-        __syncthreads();
+    // R1 <- R R1 (waves 0-3: one tile each)
+    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
+    __syncthreads();
+    {
         const int ti = w >> 1, tj = w & 1;
         Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
         if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
@@ -1091,11 +1126,157 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a) {
             W.r1[i2 * 32 + c] = i2 <= c ? rt[g] : 0.0;
         }
     }
-    cqr_gram_partial(L, x, W.gp3 + (size_t)wg * 1024);
+    // the whole Gram as partial 0, the other partials zero
+    __syncthreads();
+    double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);
+    const int qq = lane >> 4, l15 = lane & 15;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int rr = Mf<double>::crow(qq, g);
+        gw[w][rr][l15] = gacc[0][g];
+        gw[w][rr][16 + l15] = gacc[1][g];
+        gw[w][16 + l15][rr] = gacc[1][g];
+        gw[w][16 + rr][16 + l15] = gacc[2][g];
+    }
+    __syncthreads();
+    for (int el = tid; el < 1024; el += kCT) {
+        const int i2 = el >> 5, t = el & 31;
+        W.gp3[el] = (gw[0][i2][t] + gw[1][i2][t]) + (gw[2][i2][t] + gw[3][i2][t]);
+        for (int k = 1; k < nwg; ++k) W.gp3[(size_t)k * 1024 + el] = 0.0;
+    }
+}
+
+// --------------------------------------------------------------------------
+// cqr_finish: the rest of a panel's reconstruction, run by the first
+// workgroup of the read pass that follows the panel (k_rpass), beside the
+// pass itself -- the read pass uses V' = Q (the modified LU's signs enter
+// only V's top block, and Y_j = A^T V_j T_j is corrected by prep).  Wave 0:
+// the modified LU of Q_t - S = L U (s_j = -sign of the pivot); then wave 1
+// U^-1, wave 2 L^-1, wave 3 the band block R = S R' in place; then every
+// wave one tile of T = -S (U^-1 L^-1)^T.  A zero panel gets S = -I, T = 0.
+// All 512 threads of the workgroup pass the barriers; waves 4-7 idle.
+// --------------------------------------------------------------------------
+struct FinArgs {
+    const double *qt;     // Q_t (32 x 32, row-major)
+    const double *zero;   // 1: the panel was zero
+    double *sgn;          // out: s_j
+    void *tout;           // out: T
+    void *apan; long asi, ast;   // the band block R' (in place -> S R')
+};
+struct FinLds {
+    double u[32][kSP];       // U (upper)
+    double tq[32][kSP];      // Q_t, then L (strict lower)
+    double ui[32][kSP];      // U^-1
+    double li[32][kSP];      // L^-1
+    double sgn[32];
+};
+
+// (LDS matrices passed separately: k_cqr_v's inline use maps them onto its
+// own; tq_loaded: Q_t is already in tq)
+template <typename T>
+__device__ __forceinline__ void cqr_finish(double (&Lu)[32][kSP], double (&Ltq)[32][kSP], double (&Lui)[32][kSP],
+                                           double (&Lli)[32][kSP], double *Lsgn, const FinArgs &f, int tid,
+                                           bool tq_loaded) {
+    const int lane = tid & 63, w = tid >> 6;
+    const bool zero = f.zero[0] != 0.0;
+    if (!tq_loaded)
+        for (int el = tid; el < 1024; el += blockDim.x) Ltq[el >> 5][el & 31] = f.qt[el];
+    __syncthreads();
+    if (w == 0) {
+        const int r = lane & 31;
+        double rv[32];
+#pragma unroll
+        for (int cc = 0; cc < 32; ++cc) rv[cc] = Ltq[r][cc];
+        if (!zero) {
+            lu_wave(rv, Lsgn, lane);
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 32; ++jj) rv[jj] = r == jj ? 1.0 : 0.0;
+            if (lane < 32) Lsgn[lane] = -1.0;
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int cc = 0; cc < 32; ++cc) Lu[r][cc] = cc >= r ? rv[cc] : 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 32; ++cc) Ltq[r][cc] = cc < r ? rv[cc] : 0.0;
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+        if (lane < 32) f.sgn[lane] = Lsgn[lane];
+    } else if (w == 1) {
+        // U^-1 (lane c = column c, right-looking back substitution)
+        const int c = lane & 31;
+        double acc[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 31; k >= 0; --k) {
+            const double d = Lu[k][k];
+            double inv = __builtin_amdgcn_rcp(d);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            const double xk = acc[k] * inv;
+            acc[k] = xk;
+#pragma unroll
+            for (int i2 = 0; i2 < k; ++i2) acc[i2] = fma(-Lu[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) Lui[k][c] = acc[k];
+        }
+    } else if (w == 2) {
+        // L^-1 (unit lower; lane c = column c, forward substitution)
+        const int c = lane & 31;
+        double acc[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const double xk = acc[k];
+#pragma unroll
+            for (int i2 = k + 1; i2 < 32; ++i2) acc[i2] = fma(-Ltq[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) Lli[k][c] = acc[k];
+        }
+    } else if (w == 3) {
+        // R = S R' (upper block, rows scaled by s_i)
+        T *ap = (T *)f.apan;
+        for (int el = lane; el < 1024; el += 64) {
+            const int i2 = el >> 5, c = el & 31;
+            if (i2 <= c) {
+                T *pp = ap + (size_t)i2 * f.asi + (size_t)c * f.ast;
+                *pp = (T)(Lsgn[i2] * (double)*pp);
+            }
+        }
+    }
+    __syncthreads();
+    if (w < 4) {
+        // T = -S (U^-1 L^-1)^T: wave w forms tile (w >> 1, w & 1) of U^-1 L^-1
+        const int ti = w >> 1, tj = w & 1;
+        const Mf<double>::v4 pt = tile_mm(Lui, Lli, ti, tj, lane, 16 * (ti > tj ? ti : tj), 32);
+        T *tout = (T *)f.tout;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), j2 = 16 * tj + (lane & 15);
+            tout[j2 * 32 + i2] = (T)(zero ? 0.0 : -Lsgn[j2] * pt[g]);
+        }
+    }
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr_v(CqrArgs a) {
+__device__ void cqr_finish_entry(const FinArgs &f, int tid) {
+    __shared__ FinLds FL;
+    cqr_finish<T>(FL.u, FL.tq, FL.ui, FL.li, FL.sgn, f, tid, false);
+}
+
+// INLINE (the last LQ panel of a block, whose U's top block the block update
+// reads straight away): workgroup 0 also runs cqr_finish itself and patches
+// V's top block to Q_t - S in place.
+template <typename T, bool INLINE>
+__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr_v(CqrArgs a, FinArgs fin) {
     __shared__ CqrLds L;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
     CqrWs W(a.ws);
@@ -1201,7 +1382,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
             }
         }
     };
-    store_v(x, 32, INT_MAX);
+    store_v(x, 0, INT_MAX);   // V' = Q (the top rows get - S after the LU: k_vsum)
     {   // zeros below the panel's R block
         typedef typename G2<T>::v2 v2;
         if (a.ast == 1) {
@@ -1219,75 +1400,18 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wg != 0) return;
 
-    // ---- workgroup 0: the modified LU of Q_t - S, V's top rows, T and R -------
-    lds_barrier();   // L.tq complete (the V stores above need not drain)
-    if (w == 0) {
-        const int r = lane & 31;
-        double rv[32];
+    // ---- workgroup 0: Q_t and the zero flag for the LU (k_rpass's finishing
+    // workgroup), and R' = R2 R1 2^e into the panel (its rows get S there) ----
+    if (tid < 32) {
 #pragma unroll
-        for (int cc = 0; cc < 32; ++cc) rv[cc] = L.tq[r][cc];
-        if (!zero) {
-            lu_wave(rv, L.sgn, lane);
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < 32; ++jj) rv[jj] = r == jj ? 1.0 : 0.0;
-            if (lane < 32) L.sgn[lane] = -1.0;
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int cc = 0; cc < 32; ++cc) L.u[r][cc] = cc >= r ? rv[cc] : 0.0;   // U (upper)
-#pragma unroll
-            for (int cc = 0; cc < 32; ++cc) L.tq[r][cc] = cc < r ? rv[cc] : 0.0;   // L (strict lower)
-        }
-    } else if (w == 3) {
-        for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
+        for (int t = 0; t < 32; ++t) W.qt[tid * 32 + t] = x[t];
     }
-    lds_barrier();
-    if (w == 0) {
-        // V's top rows: Q_t - S
-        double v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = x[t] - (t == lane ? L.sgn[t] : 0.0);
-        store_v(v, 0, 32);
-    } else if (w == 1) {
-        // U^-1 (lane c = column c, right-looking back substitution) -> L.r1w
-        const int c = lane & 31;
-        double acc[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 31; k >= 0; --k) {
-            const double d = L.u[k][k];
-            double inv = __builtin_amdgcn_rcp(d);
-            inv = fma(inv, fma(-d, inv, 1.0), inv);
-            inv = fma(inv, fma(-d, inv, 1.0), inv);
-            const double xk = acc[k] * inv;
-            acc[k] = xk;
-#pragma unroll
-            for (int i2 = 0; i2 < k; ++i2) acc[i2] = fma(-L.u[i2][k], xk, acc[i2]);
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) L.r1w[k][c] = acc[k];
-        }
-    } else if (w == 2) {
-        // L^-1 (unit lower; lane c = column c, forward substitution) -> L.mm
-        const int c = lane & 31;
-        double acc[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            const double xk = acc[k];
-#pragma unroll
-            for (int i2 = k + 1; i2 < 32; ++i2) acc[i2] = fma(-L.tq[i2][k], xk, acc[i2]);
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) L.mm[k][c] = acc[k];
-        }
-    } else {
-        // R = S R2 R1 2^e into the panel (matrix cores, four tiles)
+    if (tid == 0) W.zero[0] = zero ? 1.0 : 0.0;
+    if (w == 3) {
+        for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4) {
             const int ti = t4 >> 1, tj = t4 & 1;
@@ -1296,23 +1420,26 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
-                ap[(size_t)i2 * a.asi + (size_t)c * a.ast] = (T)(i2 <= c ? ldexp(rt[g] * L.sgn[i2], e) : 0.0);
+                ap[(size_t)i2 * a.asi + (size_t)c * a.ast] = (T)(i2 <= c ? ldexp(rt[g], e) : 0.0);
             }
         }
     }
-    lds_barrier();
-    // T = -S (U^-1 L^-1)^T: wave w forms tile (w >> 1, w & 1) of U^-1 L^-1
-    {
-        const int ti = w >> 1, tj = w & 1;
-        const Mf<double>::v4 pt = tile_mm(L.r1w, L.mm, ti, tj, lane, 16 * (ti > tj ? ti : tj), 32);
-        T *tout = (T *)a.tout;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), j2 = 16 * tj + (lane & 15);
-            tout[j2 * 32 + i2] = (T)(zero ? 0.0 : -L.sgn[j2] * pt[g]);
+    if constexpr (INLINE) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // R' and Q_t stores landed (read back below)
+        __syncthreads();
+        cqr_finish<T>(L.u, L.tq, L.r1w, L.mm, L.sgn, fin, tid, true);
+        __syncthreads();
+        if (tid < 32) {   // V's top block: Q_t - S on the diagonal, both copies
+            T *p1 = vd + (size_t)tid * a.vsi + (size_t)tid * a.vst;
+            *p1 = (T)((double)*p1 - L.sgn[tid]);
+            if (vd2) {
+                T *p2 = vd2 + (size_t)tid * a.vsi2 + (size_t)tid * a.vst2;
+                *p2 = (T)((double)*p2 - L.sgn[tid]);
+            }
         }
     }
 }
+
 
 // ==========================================================================
 // k_blkupd: C[r][c] -= sum_{k < 256} Lw[r][k] RwT[k][c] for r >= r0, c >= c0:
@@ -1441,7 +1568,7 @@ using namespace blk;
 // device buffer: Lw m x 256, RwT 256 x ldr, partials, Qp, virtual partials
 // and result, T/S factors, cluster scratch (doubles) and counters (ints).
 struct BlkLayout {
-    size_t lw, rwt, ub, part, vpart, vout, qp, tf, cws, ctr, total;
+    size_t lw, rwt, ub, part, vpart, vout, qp, tf, cws, ctr, sg, total;
     long ldr, mp;
     int ksmax, cwg;
 };
@@ -1464,6 +1591,7 @@ static BlkLayout blk_layout(int m, int n, size_t elem) {
     L.tf = take((size_t)8 * 1024 * elem);
     L.cws = take(cqr_ws_doubles() * sizeof(double));
     L.ctr = take(64 * sizeof(int));
+    L.sg = take((size_t)(2 * NBMAX + 1) * 32 * sizeof(double));   // s_j per panel and side; zeros
     L.total = off;
     return L;
 }
@@ -1494,7 +1622,8 @@ static void blk_launch(const char *kind, double flops, double bytes, F kernel, d
 template <typename T>
 static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
                                long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
-                               int target, int *ksplit_out) {
+                               int target, int *ksplit_out, const FinArgs *fin, T *pbase, long pstride,
+                               const double *psgn) {
     RpArgs a;
     a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
     a.K = K; a.M = M;
@@ -1512,22 +1641,24 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.vpart = ws + Ly.vpart; a.vout = ws + Ly.vout;
     a.counter = counter;
     a.err = err;
+    a.has_fin = fin ? 1 : 0;
+    const FinArgs fa = fin ? *fin : FinArgs{};
     *ksplit_out = ks;
-    dim3 grid(a.nvirt + a.mtiles * ks), block(kRT);
+    dim3 grid(a.has_fin + a.nvirt + a.mtiles * ks), block(kRT);
     // algorithmic: the K x M source read once, 2 x 32 flops per element
     const double fl = 2.0 * 32 * K * M, by = (double)K * M * sizeof(T);
-    if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true>, grid, block, s, a);
-    else    blk_launch("s1_rpass", fl, by, k_rpass<T, false>, grid, block, s, a);
+    if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true, FinArgs>, grid, block, s, a, fa);
+    else    blk_launch("s1_rpass", fl, by, k_rpass<T, false, FinArgs>, grid, block, s, a, fa);
     if (a.nvirt > 0)
         blk_launch("s1_prep", 0.0, 0.0, k_vsum<T>, dim3(32 * kMT / 256), dim3(256), s, (const T *)a.vpart, (T *)a.vout,
-                   a.nvirt);
+                   a.nvirt, pbase, pstride, psgn);
     return hipGetLastError();
 }
 
 template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
-                             hipStream_t s) {
+                             hipStream_t s, bool inl, const FinArgs &fin) {
     CqrArgs a;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
@@ -1539,8 +1670,9 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.err = err;
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a);
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a);
-    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q2<T>, dim3(nwg), dim3(kCT), s, a);   // returns at once unless shifted
-    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T>, dim3(nwg), dim3(kCT), s, a);
+    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q2<T>, dim3(1), dim3(kCT), s, a, nwg);   // returns at once unless shifted
+    if (inl) blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, true>, dim3(nwg), dim3(kCT), s, a, fin);
+    else     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, false>, dim3(nwg), dim3(kCT), s, a, fin);
     return hipGetLastError();
 }
 
@@ -1555,9 +1687,24 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     T *tf = (T *)(ws + Ly.tf);   // T_j at tf + 1024 j, S_j at tf + 1024 (4 + j)
     int *ctr = (int *)(ws + Ly.ctr);
     const long ldr = Ly.ldr;
-    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);   // the read passes' last-arriver counters
+    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);
     if (e != hipSuccess) return e;
+    double *sgq = (double *)(ws + Ly.sg), *sgl = sgq + NBMAX * 32, *sg0 = sgq + 2 * NBMAX * 32;
+    e = hipMemsetAsync(sg0, 0, 32 * sizeof(double), s);   // "no correction"
+    if (e != hipSuccess) return e;
+    const double *cws = (const double *)(ws + Ly.cws);
+    // A panel's reconstruction finishes (modified LU, T, the band block's
+    // signs) in the first workgroup of the read pass that follows it, which
+    // uses V' = Q; the last LQ panel of a block finishes inline (the block
+    // update reads its U straight away).
+    auto fin_of = [&](double *sg, T *tout, T *apan, long asi, long ast) {
+        FinArgs f;
+        f.qt = cws + cqr_ws_qt(); f.zero = cws + cqr_ws_zero(); f.sgn = sg;
+        f.tout = tout; f.apan = apan; f.asi = asi; f.ast = ast;
+        return f;
+    };
     int ks_x = 1;
+    const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
             const int c = k0 + 32 * j;
@@ -1565,9 +1712,10 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             const int n2 = n - c - 32;     // columns right of it
             T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
             // ---- QR of the column panel --------------------------------------
+            const FinArgs fq = fin_of(sgq + 32 * j, Tj, A + (size_t)c * lda + c, lda, 1);
             if (j == 0) {
                 e = launch_cqr<T>(A + (size_t)c * lda + c, lda, 1, mr, Lw + (size_t)c * 256, 256, 1, nullptr, 0, 0, Tj,
-                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s);
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq);
             } else {
                 PrepArgs p;
                 p.A = A; p.lda = lda; p.Lw = Lw; p.RwT = RwT; p.ldr = ldr;
@@ -1575,17 +1723,19 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.G = ws + Ly.vout; p.Tm = tf + 1024 * (NBMAX + j - 1);
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
+                p.sgn = sg_prev;
                 blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((mr + kPI - 1) / kPI), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 32, 1, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
-                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s);
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq);
             }
             if (e != hipSuccess) return e;
-            // ---- Y pass + LQ of the row panel ----------------------------------
+            // ---- Y pass (+ the QR panel's finish) + LQ of the row panel -------
             int ks_y = 1;
             e = launch_rpass<T>(true, A + (size_t)c * lda + c + 32, lda, mr, n2, Lw + (size_t)c * 256 + 32 * j, 256,
-                                Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y);
+                                Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
+                                Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j);
             if (e != hipSuccess) return e;
             {
                 PrepArgs p;
@@ -1594,18 +1744,24 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.G = ws + Ly.vout; p.Tm = Tj;
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
+                p.sgn = sgq + 32 * j;
                 blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, dim3((n2 + kPI - 1) / kPI), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
+            const bool inl = j == NBMAX - 1;
+            const FinArgs fl = fin_of(sgl + 32 * j, Sj, A + (size_t)c * lda + c + 32, 1, lda);
             e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, n2, RwT + (size_t)(128 + 32 * j) * ldr + c + 32, 1, ldr,
-                              Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s);
+                              Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s,
+                              inl, fl);
             if (e != hipSuccess) return e;
-            // ---- X pass ----------------------------------------------------------
+            // ---- X pass (+ the LQ panel's finish) --------------------------------
             e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,
                                 Ub + (size_t)(c + 32) * 32, 32, RwT + c + 32, ldr, ws, Ly, ctr + 16, err, s,
-                                target, &ks_x);
+                                target, &ks_x, inl ? nullptr : &fl,
+                                inl ? nullptr : RwT + (size_t)(128 + 32 * j) * ldr + c + 32, ldr + 1, sgl + 32 * j);
             if (e != hipSuccess) return e;
+            sg_prev = inl ? sg0 : sgl + 32 * j;
         }
         // ---- block end: X_3, then the rank-256 update ---------------------------
         const int k1 = k0 + NBMAX * 32;
@@ -1616,6 +1772,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.G = ws + Ly.vout; p.Tm = tf + 1024 * (2 * NBMAX - 1);
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
+            p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
             blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((m - k1 + kPI - 1) / kPI), dim3(kPT), s, p);
             e = hipGetLastError();
             if (e != hipSuccess) return e;

@@ -53,5 +53,8 @@ if len(sys.argv) > 4:
         g = gui.get(k, [1, 0.0])[1] / max(gui.get(k, [1, 0.0])[0], 1)
         wall = g / 8.0
         util = b / (wall * 1024.0) if wall > 0 else 0.0
-        short = k.split("(")[0].split("::")[-1].replace(" ", "")[:55]   # e.g. k_blkupd<double>
+        head = k.split("(")[0]
+        base = head.split("<")[0].split("::")[-1]                    # e.g. k_rpass
+        targs = head[len(head.split("<")[0]):].replace("brd::blk::", "").replace(" ", "")
+        short = (base + targs)[:55]                                  # e.g. k_rpass<double,true,FinArgs>
         print(f"MFMA {short:55s} {n:6d} {mo / n * 512 / 1e9:11.3f} {b / 1e6:10.3f} {wall / 1e3:10.1f} {util:7.4f}")

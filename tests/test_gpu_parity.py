@@ -484,3 +484,31 @@ def test_release_stream_frees_and_keeps_working(S):
     M2 = A.clone()
     S.ge2band(M2, 32)
     assert torch.equal(band, M2)
+
+
+def test_reduce_many_stage2_bitwise_under_contention(S):
+    """Regression for the stage-2 hand-off protocol ("The round-2
+    sigma failure"): eight matrices through reduce_many on four lanes (four
+    sweep chains beside three stage-1 streams, every CU busy) must give the
+    bidiagonal of the serial sweep on the same band BIT FOR BIT, in both
+    geometries -- the window arithmetic does not depend on which workgroup
+    runs a bundle or when, so any difference is a hand-off (rows_done /
+    loaded publication, ring-slot reuse) fault."""
+    import torch
+    rng = np.random.default_rng(97)
+    n, b, k = 1536, 32, 8
+    As = [torch.from_numpy(rng.uniform(0, 5, (n, n))).cuda() for _ in range(k)]
+    bands = []
+    for A in As:
+        M = A.clone()
+        S.ge2band(M, b)
+        bands.append(M)
+    for sigma in (False, True):
+        ref = []
+        for Bd in bands:
+            W = Bd.clone()
+            d, e = S.band2bd(W, b, sigma=sigma)
+            ref.append((d.clone(), e.clone()))
+        got = S.reduce_many([A.clone() for A in As], b, sigma=sigma, lanes=4)
+        for (d0, e0), (d1, e1) in zip(ref, got):
+            assert torch.equal(d0, d1) and torch.equal(e0, e1)

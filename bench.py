@@ -97,6 +97,9 @@ def parse():
     p.add_argument("--stages", choices=["12", "1", "2"], default="12",
                    help="developer diagnostic: run only stage 1 or only stage 2 inside each step "
                         "(the line is then labelled, and is not the metric)")
+    p.add_argument("--same-n", choices=["on", "off"], default="on",
+                   help="N > 1 (dist): also time the one-GPU stream at the same size on rank 0 "
+                        "(single_gpu_same_n in the line)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the distributed path even at world size 1 (launch through torch.distributed.run)")
     return p.parse_args()
@@ -362,6 +365,45 @@ def maybe_spawn(args) -> None:
     sys.exit(subprocess.call(cmd, env=env))
 
 
+def single_gpu_same_n(S, torch, dev, n, b, tdt, steps, warmup, lanes, s2_cus, sigma):
+    """The one-GPU stream of reductions at this n, timed on this rank alone
+    (the same lanes / stage-2 reservation as the one-GPU bench): the
+    denominator of a like-for-like multi-GPU efficiency at the multi-GPU
+    default size."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
+    mats = [base.clone() for _ in range(warmup + steps)]
+    del base
+    sa = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    sb = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    S.set_overlap(s2_cus)
+
+    def issue(first, count):
+        for i in range(count):
+            j = first + i
+            with torch.cuda.stream(sa[j % lanes]):
+                S.ge2band(mats[j], b, sync=False)
+                e1 = torch.cuda.Event()
+                e1.record(sa[j % lanes])
+            with torch.cuda.stream(sb[j % lanes]):
+                sb[j % lanes].wait_event(e1)
+                S.band2bd(mats[j], b, sigma=sigma, sync=False, extract=False)
+    issue(0, warmup)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    issue(warmup, steps)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    S.check_errors()
+    for s_ in sa + sb:
+        S.release_stream(s_)
+    del mats
+    torch.cuda.empty_cache()
+    return {"value": round(steps * 8.0 / 3.0 * n ** 3 / el / 1e9, 2), "ms_per_step": round(el / steps * 1e3, 3),
+            "n": n, "lanes": lanes, "steps": steps}
+
+
 def main():
     args = parse()
     if args.lanes is None:
@@ -591,6 +633,18 @@ def main():
     flops_per = 8.0 / 3.0 * n ** 3
     matrices = 1 if (world == 1 or dist_mode) else world   # matrices reduced per step, whole job
     value = matrices * args.steps * flops_per / elapsed / 1e9
+    # across GPUs: the one-GPU stream at the same n on rank 0 (the others wait),
+    # so the line carries a like-for-like 1 -> N efficiency at this size
+    same_n = None
+    rehearse = os.environ.get("BRD_BENCH_SAME_N") == "1"   # world-1 rehearsal (--force-dist)
+    if (world > 1 or rehearse) and dist_mode and args.comm == "rccl" and args.same_n == "on":
+        if rank == 0:
+            try:
+                same_n = single_gpu_same_n(S, torch, dev, n, b, tdt, args.steps, max(1, args.warmup), lanes,
+                                           S.overlap_cus(n), args.s2 == "sigma")
+            except Exception as e:   # reported, never fatal to the multi-GPU line
+                same_n = {"value": None, "error": str(e)[:200]}
+        dist.barrier()
     if rank == 0:
         out = {
             "metric": METRIC if args.stages == "12" else f"DIAGNOSTIC stage {args.stages} only (not the metric)",
@@ -652,6 +706,10 @@ def main():
             "stage1_path": "blocked (delayed two-sided update, brd_stage1_blk.hip) + per-panel tail" if blocked
                            else "per-panel (brd_stage1.hip)",
         }
+        if same_n is not None:
+            out["single_gpu_same_n"] = same_n
+            out["efficiency_vs_single_gpu_same_n"] = (round(value / (world * same_n["value"]), 4)
+                                                      if same_n.get("value") else None)
         if args.cpu_baseline == "auto":
             try:
                 out["cpu_baseline"] = cpu_baseline([int(x) for x in args.cpu_n.split(",")], b, n)

@@ -87,7 +87,10 @@ constexpr int NBMAX = 4;    // panels per block (Lw / RwT hold 2 NBMAX 32 = 256 
 constexpr int kRT = 512;    // threads: 4 column waves x 2 halves of the workgroup's K range
 constexpr int kWM = 64;     // m per wave
 constexpr int kMT = 256;    // m per workgroup
-constexpr int kSU = 8;      // K steps in flight (Y); X: kSU / 2 step pairs
+#ifndef BRD_BLK_KSU
+#define BRD_BLK_KSU 8       // A/B knob (tools/variant_lib.sh)
+#endif
+constexpr int kSU = BRD_BLK_KSU;   // K steps in flight (Y); X: kSU / 2 step pairs
 
 struct RpArgs {
     const void *src;  long ld;      // source S
@@ -1459,6 +1462,7 @@ struct GemmArgs {
     const void *Lw; const void *RwT; long ldr;
     int K;                          // 256
     int tiles_c;                    // column tiles
+    int ntiles;                     // tiles (the grid may be padded)
 };
 
 template <typename T>
@@ -1474,7 +1478,29 @@ __global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
     __shared__ GemmLds<T> L;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l15 = lane & 15;
-    const int tr = blockIdx.x / a.tiles_c, tc = blockIdx.x % a.tiles_c;
+#ifndef BRD_BLK_SWZ
+#define BRD_BLK_SWZ 0   // A/B knob: > 0 = tile order in groups of that many tile rows per XCD
+#endif
+    int tr, tc;
+    if constexpr (BRD_BLK_SWZ > 0) {
+        // XCD-aware order: workgroup b runs on XCD b % 8 (dispatch round-robin);
+        // each XCD takes its own contiguous eighth of the tiles and walks them
+        // in groups of BRD_BLK_SWZ tile rows, sweeping the columns, so a group's
+        // Lw rows and the current RwT column tile stay in that XCD's L2
+        // (the grid is padded to a multiple of 8; the padding workgroups exit)
+        const int nt = a.ntiles, per = (int)gridDim.x / 8;
+        const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+        const int tt = xcd * per + loc;
+        if (tt >= nt) return;
+        const int tiles_r = nt / a.tiles_c;
+        const int G = BRD_BLK_SWZ, grp = tt / (G * a.tiles_c), rem = tt % (G * a.tiles_c);
+        const int gr = min(G, tiles_r - grp * G);
+        tr = grp * G + rem % gr;
+        tc = rem / gr;
+    } else {
+        tr = blockIdx.x / a.tiles_c;
+        tc = blockIdx.x % a.tiles_c;
+    }
     const int r0 = tr * kGM, c0 = tc * kGM;
     const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
     T *C = (T *)a.C;
@@ -1785,10 +1811,12 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             g.K = 256;
             g.tiles_c = (g.cols + kGM - 1) / kGM;
             const int tiles_r = (g.rows + kGM - 1) / kGM;
+            g.ntiles = tiles_r * g.tiles_c;
+            const int grid = BRD_BLK_SWZ > 0 ? (g.ntiles + 7) / 8 * 8 : g.ntiles;
             // algorithmic: C read and written once, Lw / RwT read once; 2 x 256 flops per element
             const double el = (double)g.rows * g.cols;
             blk_launch("s1_blkupd", 2.0 * 256 * el, (2.0 * el + 256.0 * (g.rows + g.cols)) * sizeof(T), k_blkupd<T>,
-                       dim3(tiles_r * g.tiles_c), dim3(kGT), s, g);
+                       dim3(grid), dim3(kGT), s, g);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

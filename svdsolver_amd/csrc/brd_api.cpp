@@ -438,17 +438,22 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
 }
 
 // Blocked stage 1 (brd_stage1_blk.hip) for b = 32 -- the delayed two-sided
-// update -- over all but the last panels (the default); BRD_S1_BLOCKED=0
-// keeps the per-panel path throughout (A/B and parity against the per-panel
-// kernels).
-static bool blocked_enabled() {
+// update -- over all but the last panels: the default in fp64.  In fp32 the
+// per-panel path stays the default: the blocked path's panel QR computes in
+// fp64 whatever the input type, so its latency chain costs the same while the
+// per-panel update moves half the bytes (N = 8192: stage 1 63.6 ms blocked vs
+// 59.3 per-panel; fp64 80.8 vs 86.3, 16384 fp64 366 vs 485).
+// BRD_S1_BLOCKED=1 / 0 forces either path (A/B and parity tests).
+static bool blocked_enabled(size_t elem) {
     const char *env = getenv("BRD_S1_BLOCKED");   // read per call: tests switch it between calls
-    return !(env && env[0] == '0');
+    if (env && env[0] == '0') return false;
+    if (env && env[0] == '1') return true;
+    return elem == sizeof(double);
 }
 
 template <typename T>
 static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s, bool *used_blocked = nullptr) {
-    const bool blk_ok = blocked_enabled() && b == 32 && lda % 2 == 0 && ((uintptr_t)A % 16) == 0;
+    const bool blk_ok = blocked_enabled(sizeof(T)) && b == 32 && lda % 2 == 0 && ((uintptr_t)A % 16) == 0;
     const int kend = blk_ok ? blk_columns(m, n, b) : 0;
     size_t need = tree_ws_bytes(make_tree(m, std::min(b, n)), sizeof(T));
     need = std::max(need, tree_ws_bytes(make_tree(std::max(n - 1, 1), std::min(b, n)), sizeof(T)));

@@ -330,6 +330,9 @@ constexpr int kQP = 40;    // QR pitch (rows k, k + 2 in opposite bank halves)
 
 template <typename T>
 __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
+#if BRD_DIAG_PREP == 1
+    return;
+#endif
     typedef typename Mf<T>::v4 v4;
     __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
     __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
@@ -343,35 +346,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     T *RwT = (T *)a.RwT;
     // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
     // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
-    // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
-    if (tid < nk1) {
-        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
-    }
-    if (tid < nk2) {
-        const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
-    }
-    {
-        T v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = tid + kPT * u;
-            Tt[(e & 31) * 34 + (e >> 5)] = v[u];
-        }
-    }
-    __syncthreads();
-
+    // the operands first (their latency under the staging loads)
     const int i0 = blockIdx.x * kPI + 16 * w;
     const int il = i0 + l15;                       // this lane's item (B operand / C column)
     const bool iv = il < a.items;
@@ -400,6 +375,38 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
         b1[s] = ok ? v1 : (T)0;
         b2[s] = ok ? v2 : (T)0;
     }
+    // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
+    if (tid < nk1) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
+    }
+    if (tid < nk2) {
+        const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
+    }
+    {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + kPT * u;
+            Tt[(e & 31) * 34 + (e >> 5)] = v[u];
+        }
+    }
+    __syncthreads();
+#if BRD_DIAG_PREP == 2
+    return;
+#endif
+
 #pragma unroll
     for (int s = 0; s < kMS; ++s) {
         if (s < 8 * j) {
@@ -487,6 +494,9 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
 
 template <typename T>
 __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
+#if BRD_DIAG_PREP == 1
+    return;
+#endif
     typedef typename Mf<T>::v4 v4;
     typedef typename G2<T>::v2 v2;
     __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
@@ -501,6 +511,32 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     const T *G = (const T *)a.G;
     const T *RwT = (const T *)a.RwT;
     T *Lw = (T *)a.Lw;
+    // the operands first (their latency under the staging loads)
+    const int i0 = blockIdx.x * kPI + 16 * w;
+    const int ia = i0 + l15;                        // A-operand row of this lane
+    const bool va = ia < a.items;
+    const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
+    const T *A = (const T *)a.A;
+    v4 ax[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}}, ap[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ic = i0 + Mf<T>::crow(q, g);
+            ap[h][g] = (a.factor && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
+        }
+    // ranges of Lw columns: [0, 32j) (compact 0) and [128, 128 + 32jp)
+    // (compact 32j); lane q takes k = 8s + 2q + e.  All A operands (16-byte
+    // pairs of the lane's row) are loaded before the first MFMA.
+    constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
+    v2 av1[kMP], av2[kMP];
+#pragma unroll
+    for (int s = 0; s < kMP; ++s) {
+        const int kl1 = min(8 * s, max(32 * j - 8, 0)) + 2 * q, kl2 = min(8 * s, max(32 * jp - 8, 0)) + 2 * q;
+        const v2 u1 = *(const v2 *)(lrow + kl1), u2 = *(const v2 *)(lrow + 128 + kl2);
+        av1[s] = (va && s < 4 * j) ? u1 : v2{(T)0, (T)0};
+        av2[s] = (va && s < 4 * jp) ? u2 : v2{(T)0, (T)0};
+    }
     // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
     if (tid < n1) {
         const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
@@ -529,32 +565,10 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
         }
     }
     __syncthreads();
+#if BRD_DIAG_PREP == 2
+    return;
+#endif
 
-    const int i0 = blockIdx.x * kPI + 16 * w;
-    const int ia = i0 + l15;                        // A-operand row of this lane
-    const bool va = ia < a.items;
-    const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
-    const T *A = (const T *)a.A;
-    v4 ax[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}}, ap[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int ic = i0 + Mf<T>::crow(q, g);
-            ap[h][g] = (a.factor && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
-        }
-    // ranges of Lw columns: [0, 32j) (compact 0) and [128, 128 + 32jp)
-    // (compact 32j); lane q takes k = 8s + 2q + e.  All A operands (16-byte
-    // pairs of the lane's row) are loaded before the first MFMA.
-    constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
-    v2 av1[kMP], av2[kMP];
-#pragma unroll
-    for (int s = 0; s < kMP; ++s) {
-        const int kl1 = min(8 * s, max(32 * j - 8, 0)) + 2 * q, kl2 = min(8 * s, max(32 * jp - 8, 0)) + 2 * q;
-        const v2 u1 = *(const v2 *)(lrow + kl1), u2 = *(const v2 *)(lrow + 128 + kl2);
-        av1[s] = (va && s < 4 * j) ? u1 : v2{(T)0, (T)0};
-        av2[s] = (va && s < 4 * jp) ? u2 : v2{(T)0, (T)0};
-    }
     auto krange = [&](const v2 (&av)[kMP], int cb, int ngrp) {
 #pragma unroll
         for (int s = 0; s < kMP; ++s) {
@@ -679,7 +693,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 // reconstruction.)  All arithmetic in fp64.  A first-pass Cholesky pivot
 // that is not positive or below 1e-7 x the largest (panel condition number
 // beyond ~1e7, where CholeskyQR2 loses orthogonality) switches the panel to
-// shifted CholeskyQR3 (k_cqr_q1's shift, k_cqr_q2's extra pass); a breakdown
+// shifted CholeskyQR3 (k_cqr_q1's shift, cqr_shifted_pass); a breakdown
 // after that sets the error word (3).
 // ==========================================================================
 constexpr int kCT = 256;
@@ -697,7 +711,7 @@ struct CqrArgs {
     int *err;
 };
 
-// scratch (doubles): the three Gram passes' partials [kCW][1024] each, the
+// scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
 // per-workgroup exponents, R1, the shifted-pass flag, and Q1's rows [kCW kCT][32]
 __host__ __device__ constexpr size_t cqr_ws_doubles() {
     return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
@@ -707,9 +721,9 @@ __host__ __device__ constexpr size_t cqr_ws_doubles() {
 __host__ __device__ constexpr size_t cqr_ws_qt() { return (size_t)3 * 1024 * kCW + kCW + 1024; }
 __host__ __device__ constexpr size_t cqr_ws_zero() { return cqr_ws_qt() + 1024 + 2; }
 struct CqrWs {
-    double *gp1, *gp2, *gp3, *ew, *r1, *qt, *shifted, *zero, *q1;
+    double *gp1, *gp2, *ew, *r1, *qt, *shifted, *zero, *q1;
     __device__ explicit CqrWs(double *ws)
-        : gp1(ws), gp2(ws + 1024 * kCW), gp3(ws + 2048 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
+        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
           qt(ws + cqr_ws_qt()), shifted(ws + cqr_ws_qt() + 1024), zero(ws + cqr_ws_zero()),
           q1(ws + cqr_ws_zero() + 2) {}
 };
@@ -1024,22 +1038,26 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
     CqrWs W(a.ws);
     if (tid == 0) L.flags = 0;
-    const int e = cqr_exponent(L, W.ew, nwg, false);
     const int i = wg * kCT + tid;
     double x[32];
+    cqr_load_row<T>(a, i, x);   // in flight under the Gram sum and the Cholesky
+    const int e = cqr_exponent(L, W.ew, nwg, false);
     if (e == INT_MIN) {   // zero panel: k_cqr_v writes V = [I; 0], T = 0, R = 0
         if (wg == 0 && tid == 0) W.shifted[0] = 0.0;
         return;
     }
     gram_sum_all(L, W.gp1, L.scl, nwg);
     __syncthreads();
+#if BRD_DIAG_Q1 == 2
+    if (wg >= 0) return;
+#endif
     if (w == 0) {
         bool good = chol_wave(L.g, L.r1, L.r1w, lane);
         if (!good) {
             // an ill-conditioned panel (cond > ~1e7, e.g. numerically rank
             // deficient): the shifted Cholesky of sCQR3 (Fukaya et al. 2020),
             // G + s I with s = 11 (32 M + 32 33) u tr(G); then Q1 has
-            // cond ~ 1e3 and k_cqr_q2 re-orthogonalises it once more
+            // cond ~ 1e3 and k_cqr_v's cqr_shifted_pass re-orthogonalises it once more
             double tr = 0;
 #pragma unroll
             for (int k = 0; k < 32; ++k) tr += L.g[k][k];
@@ -1053,13 +1071,15 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
         }
     }
     __syncthreads();
+#if BRD_DIAG_Q1 == 1
+    if (wg >= 0) return;
+#endif
     if (L.flags == 1 && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wg == 0) {
         for (int el = tid; el < 1024; el += kCT) W.r1[el] = L.r1[el >> 5][el & 31];
         if (tid == 0) W.shifted[0] = L.flags == 2 ? 1.0 : 0.0;
     }
     // Q1 = (P 2^-e) R1^-1
-    cqr_load_row<T>(a, i, x);
 #pragma unroll
     for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e);
     trsm_row(x, L.r1w);
@@ -1075,62 +1095,55 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
 }
 
-// After a shifted first pass only (W.shifted; it returns at once otherwise):
-// one more CholeskyQR pass on Q1 -- Q1 <- Q1 R^-1, R1 <- R R1 -- and the
-// Gram of the new Q1 into gp3 (sCQR3's middle pass).  ONE workgroup walks all
-// rows (the rare ill-conditioned panel pays ~0.1-0.2 ms; the common case pays
-// only a one-workgroup launch instead of a panel-wide one).
-template <typename T>
-__global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a, int nwg) {
-    __shared__ CqrLds L;
-    CqrWs W(a.ws);
-    if (W.shifted[0] == 0.0) return;
+// After a shifted first pass only (W.shifted): sCQR3's middle pass, run by
+// every workgroup of k_cqr_v on its own (the same reads in the same order,
+// so the same result everywhere; no kernel of its own, which the common
+// unshifted panel would pay for as a launch): R = chol(Q1^T Q1), the Gram of
+// Q1 R^-1 over ALL rows into L.g (the four waves' sums in fixed order),
+// R R1 into L.r1 and this thread's row of Q1 R^-1 into x.  Every workgroup
+// walks all rows (the rare ill-conditioned panel pays ~0.1-0.2 ms).
+__device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, int M, int nwg, double (&x)[32]) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) L.flags = 0;
-    cqr_exponent(L, W.ew, nwg, true);
     gram_sum_all(L, W.gp2, L.scl, nwg);
     __syncthreads();
     if (w == 0) {
         const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
         if (lane == 0 && !good) L.flags = 1;
     }
+    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
     __syncthreads();
-    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     double gacc[3][4] = {};
     for (int chunk = 0; chunk < nwg; ++chunk) {
         const int i = chunk * kCT + tid;
-        double x[32];
-        d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
+        double y[32];
+        const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
 #pragma unroll
         for (int p = 0; p < 16; ++p) {
             const d2v v = q1r[p];
-            x[2 * p] = v.x;
-            x[2 * p + 1] = v.y;
+            y[2 * p] = v.x;
+            y[2 * p + 1] = v.y;
         }
-        trsm_row(x, L.r2w);
-        if (i >= a.M) {
+        trsm_row(y, L.r2w);
+        if (i >= M) {
 #pragma unroll
-            for (int t = 0; t < 32; ++t) x[t] = 0.0;
+            for (int t = 0; t < 32; ++t) y[t] = 0.0;
         }
+        if (chunk == (int)blockIdx.x) {
 #pragma unroll
-        for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
-        gram_wave(L, w, lane, x, gacc);
+            for (int t = 0; t < 32; ++t) x[t] = y[t];
+        }
+        gram_wave(L, w, lane, y, gacc);
     }
-    // R1 <- R R1 (waves 0-3: one tile each)
-    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
+    // R R1 (waves 0-3: one tile each, into registers first: L.r1 is an operand)
+    Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
+    const int ti = w >> 1, tj = w & 1;
+    if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
     __syncthreads();
-    {
-        const int ti = w >> 1, tj = w & 1;
-        Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
-        if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
-            W.r1[i2 * 32 + c] = i2 <= c ? rt[g] : 0.0;
-        }
+    for (int g = 0; g < 4; ++g) {
+        const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
+        L.r1[i2][c] = i2 <= c ? rt[g] : 0.0;
     }
-    // the whole Gram as partial 0, the other partials zero
-    __syncthreads();
     double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);
     const int qq = lane >> 4, l15 = lane & 15;
 #pragma unroll
@@ -1144,8 +1157,7 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q2(CqrArgs a, int nwg) {
     __syncthreads();
     for (int el = tid; el < 1024; el += kCT) {
         const int i2 = el >> 5, t = el & 31;
-        W.gp3[el] = (gw[0][i2][t] + gw[1][i2][t]) + (gw[2][i2][t] + gw[3][i2][t]);
-        for (int k = 1; k < nwg; ++k) W.gp3[(size_t)k * 1024 + el] = 0.0;
+        L.g[i2][t] = (gw[0][i2][t] + gw[1][i2][t]) + (gw[2][i2][t] + gw[3][i2][t]);
     }
 }
 
@@ -1291,8 +1303,19 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     T *vd = (T *)a.vdst;
     T *vd2 = (T *)a.vdst2;
     double x[32];
+    const bool sh = !zero && W.shifted[0] != 0.0;
+    if (!zero && !sh) {   // this thread's row of Q1, in flight under the Gram sum
+        const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+            const d2v v = q1r[p];
+            x[2 * p] = v.x;
+            x[2 * p + 1] = v.y;
+        }
+    }
     if (!zero) {
-        gram_sum_all(L, W.shifted[0] != 0.0 ? W.gp3 : W.gp2, L.scl, nwg);
+        if (sh) cqr_shifted_pass(L, W, a.M, nwg, x);
+        else    gram_sum_all(L, W.gp2, L.scl, nwg);
         __syncthreads();
         // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
         // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
@@ -1322,15 +1345,6 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         }
         __syncthreads();
         // Q = Q1 R2^-1, this thread's row
-        {
-            const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
-#pragma unroll
-            for (int p = 0; p < 16; ++p) {
-                const d2v v = q1r[p];
-                x[2 * p] = v.x;
-                x[2 * p + 1] = v.y;
-            }
-        }
         if (fast) umul_row(x, L.r2w);
         else      trsm_row(x, L.r2w);
         if (i >= a.M) {
@@ -1411,7 +1425,8 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     }
     if (tid == 0) W.zero[0] = zero ? 1.0 : 0.0;
     if (w == 3) {
-        for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
+        if (!sh)   // (after a shifted pass L.r1 already holds R R1)
+            for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1696,7 +1711,6 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.err = err;
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a);
     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a);
-    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q2<T>, dim3(1), dim3(kCT), s, a, nwg);   // returns at once unless shifted
     if (inl) blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, true>, dim3(nwg), dim3(kCT), s, a, fin);
     else     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, false>, dim3(nwg), dim3(kCT), s, a, fin);
     return hipGetLastError();

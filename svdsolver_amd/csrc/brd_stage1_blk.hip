@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 //   QR (item i = row c+i, c = column of panel j >= 1):
 //     x   = sum_ks part[ks][i][:] - sum_{k in K1} Lw[row][k] G[k][:]      K1 = V_<=j-1, X_<j-1
 //     X_{j-1} = x S_{j-1}        -> Lw[row][128 + 32(j-1) + t]
-//     factor: p = A[row][c+t] - sum_{k in K2} Lw[row][k] RwT[k][c+t]     K2 = V_<j, X_<j -> Qp[i][t]
+//     factor: p = A[row][c+t] - sum_{k in K2} Lw[row][k] RwT[k][c+t]     K2 = V_<j, X_<j -> QpT[t][i]
 //     (D[i][t]: the A operand Lw[row][.] is read as 16-byte pairs, two k
 //     steps each, shared by both corrections)
 // K sets are kept compact in LDS: [0, 32a) and [128, 128 + 32b) stored
@@ -315,7 +315,7 @@ struct PrepArgs {
     const void *part; long mp; int ksplit;
     const void *G;            // virtual result of the read pass (LQ: [32][256], QR: [256][32])
     const void *Tm;           // T_j (LQ) / S_{j-1} (QR), 32 x 32 row-major
-    void *Qp;                 // LQ: QpT [32][mq]; QR: Qp [rows][32]
+    void *Qp;                 // the corrected panel, transposed: QpT [32][mq] (both sides)
     long mq;
     int c;                    // panel column
     int j;                    // panel index in the block
@@ -659,14 +659,25 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) ap[h] = Mf<T>::mma(av, Rs[kk * kQP + 16 * h + l15], ap[h]);
     }
-    T *Qp = (T *)a.Qp;
+    // P^T [32][mq] (the panel QR reads a lane per row: coalesced), through the
+    // wave's transpose tile: 16 consecutive items x 4 t per store
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int ic = i0 + Mf<T>::crow(q, g);
-            if (ic < a.items) Qp[(size_t)ic * 32 + 16 * h + l15] = ap[h][g];
-        }
+        for (int g = 0; g < 4; ++g) Tb[w][Mf<T>::crow(q, g) * 34 + 16 * h + l15] = ap[h][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    T *QpT = (T *)a.Qp;
+    const bool vs = i0 + l15 < a.items;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int t = 4 * it + q;
+        if (vs) QpT[(size_t)t * a.mq + i0 + l15] = Tb[w][l15 * 34 + t];
+    }
 }
 
 // ==========================================================================
@@ -699,6 +710,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 constexpr int kCT = 256;
 constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
 constexpr int kCW = 64;   // most workgroups per panel (M <= kCW kCT rows)
+constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace ([32][kQS]: a lane per row, coalesced)
 
 struct CqrArgs {
     const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
@@ -712,7 +724,7 @@ struct CqrArgs {
 };
 
 // scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
-// per-workgroup exponents, R1, the shifted-pass flag, and Q1's rows [kCW kCT][32]
+// per-workgroup exponents, R1, the shifted-pass flag, and Q1 [32][kCW kCT]
 __host__ __device__ constexpr size_t cqr_ws_doubles() {
     return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
 }
@@ -1087,11 +1099,8 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
 #pragma unroll
         for (int t = 0; t < 32; ++t) x[t] = 0.0;
     }
-    {
-        d2v *q1r = (d2v *)(W.q1 + (size_t)i * 32);
 #pragma unroll
-        for (int p = 0; p < 16; ++p) q1r[p] = d2v{x[2 * p], x[2 * p + 1]};
-    }
+    for (int t = 0; t < 32; ++t) W.q1[t * kQS + i] = x[t];
     cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
 }
 
@@ -1116,13 +1125,8 @@ __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, int 
     for (int chunk = 0; chunk < nwg; ++chunk) {
         const int i = chunk * kCT + tid;
         double y[32];
-        const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
 #pragma unroll
-        for (int p = 0; p < 16; ++p) {
-            const d2v v = q1r[p];
-            y[2 * p] = v.x;
-            y[2 * p + 1] = v.y;
-        }
+        for (int t = 0; t < 32; ++t) y[t] = W.q1[t * kQS + i];
         trsm_row(y, L.r2w);
         if (i >= M) {
 #pragma unroll
@@ -1305,13 +1309,8 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     double x[32];
     const bool sh = !zero && W.shifted[0] != 0.0;
     if (!zero && !sh) {   // this thread's row of Q1, in flight under the Gram sum
-        const d2v *q1r = (const d2v *)(W.q1 + (size_t)i * 32);
 #pragma unroll
-        for (int p = 0; p < 16; ++p) {
-            const d2v v = q1r[p];
-            x[2 * p] = v.x;
-            x[2 * p + 1] = v.y;
-        }
+        for (int t = 0; t < 32; ++t) x[t] = W.q1[t * kQS + i];
     }
     if (!zero) {
         if (sh) cqr_shifted_pass(L, W, a.M, nwg, x);
@@ -1767,7 +1766,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((mr + kPI - 1) / kPI), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
-                e = launch_cqr<T>((const T *)(ws + Ly.qp), 32, 1, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
+                e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
                                   A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq);
             }
             if (e != hipSuccess) return e;

@@ -92,6 +92,7 @@ constexpr int kMT = 256;    // m per workgroup
 #endif
 constexpr int kSU = BRD_BLK_KSU;   // K steps in flight (Y); X: kSU / 2 step pairs
 
+constexpr int kRpLds = 8192;   // doubles
 struct RpArgs {
     const void *src;  long ld;      // source S
     const void *vsrc; long vld;     // virtual tile source (256 wide), or null
@@ -109,7 +110,7 @@ struct RpArgs {
 
 struct FinArgs;
 template <typename T>
-__device__ void cqr_finish_entry(const FinArgs &f, int tid);
+__device__ void cqr_finish_entry(const FinArgs &f, int tid, void *lds);
 
 template <typename T, bool YP, typename FA>
 __global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a, FA fin) {
@@ -117,8 +118,11 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a, FA fin) {
     typedef typename Mf<T>::v4 v4;
     const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, kh = tid >> 8;
     const int q = lane >> 4, l15 = lane & 15;
+    // one LDS block for the K halves' reduction and (workgroup 0) cqr_finish:
+    // 64 KB, so two workgroups share a CU
+    __shared__ __attribute__((aligned(16))) double rp_lds[kRpLds];
     if (a.has_fin && blockIdx.x == 0) {   // the previous panel's LU, T and R signs, beside the pass
-        cqr_finish_entry<T>(fin, tid);
+        cqr_finish_entry<T>(fin, tid, rp_lds);
         return;
     }
     const int bid = blockIdx.x - a.has_fin;
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a, FA fin) {
 
     // ---- the second half's sums into the first half's, fixed order ----------
     {
-        __shared__ T red[4][32][64];
+        T (*red)[32][64] = reinterpret_cast<T (*)[32][64]>(rp_lds);
         if (kh) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -289,7 +293,8 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 
 // ==========================================================================
 // k_prep: the per-column (LQ side) / per-row (QR side) corrections, on the
-// matrix cores.  64 items per workgroup, 16 per wave.
+// matrix cores.  32 items per workgroup, 16 per item wave, the K1 range in
+// two halves (waves w and w + 2).
 //   LQ (item i = column c+32+i of panel j, c = panel column):
 //     y   = sum_ks part[ks][:][i] - sum_{k in K1} RwT[k][col] G[k][:]     K1 = V_<j, X_<j
 //     Y_j = y T_j                -> RwT[32j + t][col]
@@ -307,7 +312,9 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 // back to back.
 // ==========================================================================
 constexpr int kPT = 256;
-constexpr int kPI = 64;    // items per workgroup
+constexpr int kPI = 32;    // items per workgroup: two item waves x two halves of the K1 range
+                           // (the correction's MFMA chain split over all four SIMDs; the
+                           // halves meet in LDS, fixed order)
 
 struct PrepArgs {
     void *A; long lda;
@@ -337,7 +344,8 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
     __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
     __shared__ T Tt[32 * 34];    // T_j^T
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ T Xh[2][16][64];  // the second K half's accumulators
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wi = w & 1, kh = w >> 1;
     const int q = lane >> 4, l15 = lane & 15;
     const int j = a.j, c = a.c;
     const int nk1 = 64 * j, nk2 = 64 * j + 32;
@@ -347,7 +355,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
     // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
     // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * kPI + 16 * w;
+    const int i0 = blockIdx.x * kPI + 16 * wi;
     const int il = i0 + l15;                       // this lane's item (B operand / C column)
     const bool iv = il < a.items;
     const long col = (long)c + 32 + il;
@@ -359,21 +367,20 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
         for (int g = 0; g < 4; ++g) {
             const int t = 16 * h + Mf<T>::crow(q, g);
             ay[h][g] = (T)0;
-            aq[h][g] = iv ? A[(size_t)(c + t) * a.lda + col] : (T)0;
+            aq[h][g] = (iv && kh == 0) ? A[(size_t)(c + t) * a.lda + col] : (T)0;
         }
     // ---- K1: both corrections share the B operand RwT[k][col] ----------------
-    // all B operands are loaded before the first MFMA (unconditional loads at
-    // clamped addresses, zeroed when out of range): one memory latency, not one per step
+    // half kh = 0 takes the V_<j part (RwT rows [0, 32j)), kh = 1 the X_<j part
+    // (rows [128, 128 + 32j)); all B operands are loaded before the first MFMA
+    // (unconditional loads at clamped addresses, zeroed when out of range)
     constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
     const long colc = iv ? col : (long)c + 32;
-    T b1[kMS], b2[kMS];
+    T bk[kMS];
 #pragma unroll
     for (int s = 0; s < kMS; ++s) {
-        const int k1 = min(4 * s + q, max(32 * j - 1, 0)), k2 = 128 + k1;
-        const T v1 = RwT[(size_t)k1 * a.ldr + colc], v2 = RwT[(size_t)k2 * a.ldr + colc];
-        const bool ok = iv && s < 8 * j;
-        b1[s] = ok ? v1 : (T)0;
-        b2[s] = ok ? v2 : (T)0;
+        const int k1 = min(4 * s + q, max(32 * j - 1, 0)) + 128 * kh;
+        const T v1 = RwT[(size_t)k1 * a.ldr + colc];
+        bk[s] = (iv && s < 8 * j) ? v1 : (T)0;
     }
     // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
     if (tid < nk1) {
@@ -407,19 +414,39 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     return;
 #endif
 
+    {
+        const int gb = kh ? 32 * j : 0, lb = kh ? 32 * j + 32 : 0;   // compact bases: V_<j | X_<j
 #pragma unroll
-    for (int s = 0; s < kMS; ++s) {
-        if (s < 8 * j) {
-            const int kk1 = 4 * s + q, kk2 = 32 * j + 4 * s + q;
+        for (int s = 0; s < kMS; ++s) {
+            if (s < 8 * j) {
+                const int kk = 4 * s + q;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + kk1], b1[s], ay[h]);
-                aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + kk1], b1[s], aq[h]);                 // V_<j
-                ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + kk2], b2[s], ay[h]);
-                aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + kk2 + 32], b2[s], aq[h]);            // X_<j
+                for (int h = 0; h < 2; ++h) {
+                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[s], ay[h]);
+                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[s], aq[h]);
+                }
             }
         }
     }
+    // the halves meet: kh = 1 hands its sums over and is done
+    if (kh) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                Xh[wi][4 * h + g][lane] = ay[h][g];
+                Xh[wi][8 + 4 * h + g][lane] = aq[h][g];
+            }
+    }
+    __syncthreads();
+    if (kh) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            ay[h][g] += Xh[wi][4 * h + g][lane];
+            aq[h][g] += Xh[wi][8 + 4 * h + g][lane];
+        }
     // ---- y = sum of split partials - correction ------------------------------
     const T *part = (const T *)a.part;
     T y[2][4];
@@ -501,8 +528,9 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     typedef typename G2<T>::v2 v2;
     __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
     __shared__ T Ss[32 * 48];        // S_{j-1}
-    __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ T Tb[2][16 * 34];     // per-wave transpose of x / X_{j-1}
+    __shared__ T Xh[2][16][64];      // the second K half's accumulators
+    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6, w = wk & 1, kh = wk >> 1;
     const int q = lane >> 4, l15 = lane & 15;
     const int j = a.j, jp = j - 1, c = a.c;
     const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
@@ -512,7 +540,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     const T *RwT = (const T *)a.RwT;
     T *Lw = (T *)a.Lw;
     // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * kPI + 16 * w;
+    const int i0 = blockIdx.x * kPI + 16 * w;     // (w: the item wave)
     const int ia = i0 + l15;                        // A-operand row of this lane
     const bool va = ia < a.items;
     const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
@@ -523,19 +551,19 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ic = i0 + Mf<T>::crow(q, g);
-            ap[h][g] = (a.factor && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
+            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
         }
-    // ranges of Lw columns: [0, 32j) (compact 0) and [128, 128 + 32jp)
-    // (compact 32j); lane q takes k = 8s + 2q + e.  All A operands (16-byte
-    // pairs of the lane's row) are loaded before the first MFMA.
+    // ranges of Lw columns: [0, 32j) (compact 0; K half 0) and [128, 128 + 32jp)
+    // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
+    // (16-byte pairs of the lane's row) are loaded before the first MFMA.
     constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
-    v2 av1[kMP], av2[kMP];
+    const int ngrp = kh ? 4 * jp : 4 * j, kcb = kh ? 32 * j : 0;
+    v2 av[kMP];
 #pragma unroll
     for (int s = 0; s < kMP; ++s) {
-        const int kl1 = min(8 * s, max(32 * j - 8, 0)) + 2 * q, kl2 = min(8 * s, max(32 * jp - 8, 0)) + 2 * q;
-        const v2 u1 = *(const v2 *)(lrow + kl1), u2 = *(const v2 *)(lrow + 128 + kl2);
-        av1[s] = (va && s < 4 * j) ? u1 : v2{(T)0, (T)0};
-        av2[s] = (va && s < 4 * jp) ? u2 : v2{(T)0, (T)0};
+        const int kl = min(8 * s, max(8 * ngrp - 8, 0)) + 2 * q + 128 * kh;
+        const v2 u = *(const v2 *)(lrow + kl);
+        av[s] = (va && s < ngrp) ? u : v2{(T)0, (T)0};
     }
     // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
     if (tid < n1) {
@@ -586,8 +614,26 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
             }
         }
     };
-    krange(av1, 0, 4 * j);              // V_<j      (K1 and K2)
-    krange(av2, 32 * j, 4 * jp);        // X_<j-1    (K1 and K2)
+    krange(av, kcb, ngrp);              // V_<j (kh = 0) | X_<j-1 (kh = 1), K1 and K2
+    // the halves meet: kh = 1 hands its sums over and is done
+    if (kh) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                Xh[w][4 * h + g][lane] = ax[h][g];
+                Xh[w][8 + 4 * h + g][lane] = ap[h][g];
+            }
+    }
+    __syncthreads();
+    if (kh) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            ax[h][g] += Xh[w][4 * h + g][lane];
+            ap[h][g] += Xh[w][8 + 4 * h + g][lane];
+        }
     // ---- x = sum of split partials - correction; X_{j-1} = x S ---------------
     const T *part = (const T *)a.part;
     T xs[2][4];
@@ -1286,8 +1332,9 @@ __device__ __forceinline__ void cqr_finish(double (&Lu)[32][kSP], double (&Ltq)[
 }
 
 template <typename T>
-__device__ void cqr_finish_entry(const FinArgs &f, int tid) {
-    __shared__ FinLds FL;
+__device__ void cqr_finish_entry(const FinArgs &f, int tid, void *lds) {
+    static_assert(sizeof(FinLds) <= kRpLds * sizeof(double), "cqr_finish's LDS exceeds the read pass's block");
+    FinLds &FL = *reinterpret_cast<FinLds *>(lds);
     cqr_finish<T>(FL.u, FL.tq, FL.ui, FL.li, FL.sgn, f, tid, false);
 }
 

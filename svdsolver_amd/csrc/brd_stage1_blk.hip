@@ -293,8 +293,8 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 
 // ==========================================================================
 // k_prep: the per-column (LQ side) / per-row (QR side) corrections, on the
-// matrix cores.  32 items per workgroup, 16 per item wave, the K1 range in
-// two halves (waves w and w + 2).
+// matrix cores.  16 items per item wave; split (PrepArgs::split): 32 items per
+// workgroup, the K1 range in two halves (waves w and w + 2); else 64 items.
 //   LQ (item i = column c+32+i of panel j, c = panel column):
 //     y   = sum_ks part[ks][:][i] - sum_{k in K1} RwT[k][col] G[k][:]     K1 = V_<j, X_<j
 //     Y_j = y T_j                -> RwT[32j + t][col]
@@ -312,9 +312,10 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 // back to back.
 // ==========================================================================
 constexpr int kPT = 256;
-constexpr int kPI = 32;    // items per workgroup: two item waves x two halves of the K1 range
-                           // (the correction's MFMA chain split over all four SIMDs; the
-                           // halves meet in LDS, fixed order)
+constexpr int kPI = 32;    // items per workgroup when split: two item waves x two halves of
+                           // the K1 range (the correction's MFMA chain over all four SIMDs;
+                           // the halves meet in LDS, fixed order); unsplit: 2 kPI items,
+                           // four item waves (when the split grid would exceed the CUs)
 
 struct PrepArgs {
     void *A; long lda;
@@ -329,6 +330,7 @@ struct PrepArgs {
     int items;
     int reduce, factor;       // QR side switches
     const double *sgn;        // s_t of the panel whose pass preceded (V' = Q was used: corrections)
+    int split;                // 1: kPI items, K1 in two halves; 0: 2 kPI items, one K range
 };
 
 constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
@@ -345,7 +347,8 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
     __shared__ T Tt[32 * 34];    // T_j^T
     __shared__ T Xh[2][16][64];  // the second K half's accumulators
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wi = w & 1, kh = w >> 1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wi = a.split ? w & 1 : w, kh = a.split ? w >> 1 : 0;
     const int q = lane >> 4, l15 = lane & 15;
     const int j = a.j, c = a.c;
     const int nk1 = 64 * j, nk2 = 64 * j + 32;
@@ -355,7 +358,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
     // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
     // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * kPI + 16 * wi;
+    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * wi;
     const int il = i0 + l15;                       // this lane's item (B operand / C column)
     const bool iv = il < a.items;
     const long col = (long)c + 32 + il;
@@ -375,13 +378,17 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     // (unconditional loads at clamped addresses, zeroed when out of range)
     constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
     const long colc = iv ? col : (long)c + 32;
-    T bk[kMS];
+    T bk[2][kMS];
 #pragma unroll
-    for (int s = 0; s < kMS; ++s) {
-        const int k1 = min(4 * s + q, max(32 * j - 1, 0)) + 128 * kh;
-        const T v1 = RwT[(size_t)k1 * a.ldr + colc];
-        bk[s] = (iv && s < 8 * j) ? v1 : (T)0;
-    }
+    for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int s = 0; s < kMS; ++s) {
+            const int k1 = min(4 * s + q, max(32 * j - 1, 0)) + 128 * pp;
+            const bool mine = a.split ? pp == kh : true;
+            T v1 = (T)0;
+            if (mine) v1 = RwT[(size_t)k1 * a.ldr + colc];
+            bk[pp][s] = (iv && s < 8 * j) ? v1 : (T)0;
+        }
     // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
     if (tid < nk1) {
         const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
@@ -410,43 +417,42 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
         }
     }
     __syncthreads();
-#if BRD_DIAG_PREP == 2
-    return;
-#endif
-
-    {
-        const int gb = kh ? 32 * j : 0, lb = kh ? 32 * j + 32 : 0;   // compact bases: V_<j | X_<j
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        if (a.split && pp != kh) continue;
+        const int gb = pp ? 32 * j : 0, lb = pp ? 32 * j + 32 : 0;   // compact bases: V_<j | X_<j
 #pragma unroll
         for (int s = 0; s < kMS; ++s) {
             if (s < 8 * j) {
                 const int kk = 4 * s + q;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[s], ay[h]);
-                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[s], aq[h]);
+                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[pp][s], ay[h]);
+                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[pp][s], aq[h]);
                 }
             }
         }
     }
-    // the halves meet: kh = 1 hands its sums over and is done
-    if (kh) {
+    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
+        if (kh) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    Xh[wi][4 * h + g][lane] = ay[h][g];
+                    Xh[wi][8 + 4 * h + g][lane] = aq[h][g];
+                }
+        }
+        __syncthreads();
+        if (kh) return;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                Xh[wi][4 * h + g][lane] = ay[h][g];
-                Xh[wi][8 + 4 * h + g][lane] = aq[h][g];
+                ay[h][g] += Xh[wi][4 * h + g][lane];
+                aq[h][g] += Xh[wi][8 + 4 * h + g][lane];
             }
     }
-    __syncthreads();
-    if (kh) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            ay[h][g] += Xh[wi][4 * h + g][lane];
-            aq[h][g] += Xh[wi][8 + 4 * h + g][lane];
-        }
     // ---- y = sum of split partials - correction ------------------------------
     const T *part = (const T *)a.part;
     T y[2][4];
@@ -528,9 +534,10 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     typedef typename G2<T>::v2 v2;
     __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
     __shared__ T Ss[32 * 48];        // S_{j-1}
-    __shared__ T Tb[2][16 * 34];     // per-wave transpose of x / X_{j-1}
+    __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
     __shared__ T Xh[2][16][64];      // the second K half's accumulators
-    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6, w = wk & 1, kh = wk >> 1;
+    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
+    const int w = a.split ? wk & 1 : wk, kh = a.split ? wk >> 1 : 0;   // item wave, K half
     const int q = lane >> 4, l15 = lane & 15;
     const int j = a.j, jp = j - 1, c = a.c;
     const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
@@ -540,7 +547,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     const T *RwT = (const T *)a.RwT;
     T *Lw = (T *)a.Lw;
     // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * kPI + 16 * w;     // (w: the item wave)
+    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * w;
     const int ia = i0 + l15;                        // A-operand row of this lane
     const bool va = ia < a.items;
     const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
@@ -557,13 +564,18 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
     // (16-byte pairs of the lane's row) are loaded before the first MFMA.
     constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
-    const int ngrp = kh ? 4 * jp : 4 * j, kcb = kh ? 32 * j : 0;
-    v2 av[kMP];
+    v2 av[2][kMP];
 #pragma unroll
-    for (int s = 0; s < kMP; ++s) {
-        const int kl = min(8 * s, max(8 * ngrp - 8, 0)) + 2 * q + 128 * kh;
-        const v2 u = *(const v2 *)(lrow + kl);
-        av[s] = (va && s < ngrp) ? u : v2{(T)0, (T)0};
+    for (int pp = 0; pp < 2; ++pp) {
+        const int ng = pp ? 4 * jp : 4 * j;
+        const bool mine = a.split ? pp == kh : true;
+#pragma unroll
+        for (int s = 0; s < kMP; ++s) {
+            const int kl = min(8 * s, max(8 * ng - 8, 0)) + 2 * q + 128 * pp;
+            v2 u = v2{(T)0, (T)0};
+            if (mine) u = *(const v2 *)(lrow + kl);
+            av[pp][s] = (va && s < ng) ? u : v2{(T)0, (T)0};
+        }
     }
     // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
     if (tid < n1) {
@@ -614,26 +626,28 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
             }
         }
     };
-    krange(av, kcb, ngrp);              // V_<j (kh = 0) | X_<j-1 (kh = 1), K1 and K2
-    // the halves meet: kh = 1 hands its sums over and is done
-    if (kh) {
+    if (!a.split || kh == 0) krange(av[0], 0, 4 * j);         // V_<j      (K1 and K2)
+    if (!a.split || kh == 1) krange(av[1], 32 * j, 4 * jp);   // X_<j-1    (K1 and K2)
+    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
+        if (kh) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    Xh[w][4 * h + g][lane] = ax[h][g];
+                    Xh[w][8 + 4 * h + g][lane] = ap[h][g];
+                }
+        }
+        __syncthreads();
+        if (kh) return;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                Xh[w][4 * h + g][lane] = ax[h][g];
-                Xh[w][8 + 4 * h + g][lane] = ap[h][g];
+                ax[h][g] += Xh[w][4 * h + g][lane];
+                ap[h][g] += Xh[w][8 + 4 * h + g][lane];
             }
     }
-    __syncthreads();
-    if (kh) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            ax[h][g] += Xh[w][4 * h + g][lane];
-            ap[h][g] += Xh[w][8 + 4 * h + g][lane];
-        }
     // ---- x = sum of split partials - correction; X_{j-1} = x S ---------------
     const T *part = (const T *)a.part;
     T xs[2][4];
@@ -1706,6 +1720,15 @@ static void blk_launch(const char *kind, double flops, double bytes, F kernel, d
         hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
 }
 
+// the prep kernels' grid: split K halves (kPI items per workgroup) while
+// that grid fits the CUs the stream may use (one workgroup per CU: LDS),
+// else 2 kPI items per workgroup, one K range per wave
+static dim3 prep_grid(PrepArgs &p, int cus) {
+    const int n1 = (p.items + kPI - 1) / kPI;
+    p.split = n1 <= cus ? 1 : 0;
+    return dim3(p.split ? n1 : (p.items + 2 * kPI - 1) / (2 * kPI));
+}
+
 template <typename T>
 static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
                                long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
@@ -1810,7 +1833,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
-                blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((mr + kPI - 1) / kPI), dim3(kPT), s, p);
+                blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, prep_grid(p, target), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -1831,7 +1854,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
-                blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, dim3((n2 + kPI - 1) / kPI), dim3(kPT), s, p);
+                blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, prep_grid(p, target), dim3(kPT), s, p);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -1859,7 +1882,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
-            blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, dim3((m - k1 + kPI - 1) / kPI), dim3(kPT), s, p);
+            blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, prep_grid(p, target), dim3(kPT), s, p);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -962,8 +962,10 @@ __device__ __forceinline__ void trsm_row(double (&x)[32], const double (&Rw)[32]
 #pragma unroll
             for (int p = (k + 1) / 2; p < 16; ++p) cur[p] = nxt[p];
         }
+#ifndef BRD_TRSM_FREE   // A/B knob: 1 = no scheduling groups (the compiler's own order)
         __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // the next row's LDS reads first
         __builtin_amdgcn_sched_group_barrier(0x2, 64, 0);     // then this step's VALU
+#endif
     }
 }
 

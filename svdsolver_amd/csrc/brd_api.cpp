@@ -123,6 +123,10 @@ struct Ctx {
         // gives up, never reset by a launch (an asynchronous call's failure
         // stays visible until a synchronous call or brd_check_errors reads it).
         int *s2_err = nullptr;
+        // Stage-1 error word (blocked path: 3 = CholeskyQR breakdown), kept
+        // apart from stage 2's so a sync stage-1 call never consumes (and
+        // misreports) a code an earlier asynchronous stage 2 left.
+        int *s1_err = nullptr;
         void *stage = nullptr;       // host-pointer calls: cached HBM staging buffer
         size_t stage_bytes = 0;
     };
@@ -195,19 +199,33 @@ static int ensure_s2_flags(int n, int **out, int **err) {
     return BRD_OK;
 }
 
-// Reads (and clears) a slot's stage-2 error word; the slot's stream is drained.
-static int take_s2_error(Ctx::Slot &w, int *code) {
+static int ensure_s1_err(int **err) {
+    Ctx::Slot &w = slot();
+    if (!g_ctx.s2_err_host && hipHostMalloc(&g_ctx.s2_err_host, sizeof(int)) != hipSuccess)
+        return fail(BRD_ENOMEM, "pinned allocation failed");
+    if (!w.s1_err) {
+        if (hipMalloc(&w.s1_err, sizeof(int)) != hipSuccess) return fail(BRD_ENOMEM, "stage-1 error word allocation failed");
+        if (hipMemsetAsync(w.s1_err, 0, sizeof(int), w.s) != hipSuccess) return fail(BRD_EHIP, "stage-1 error word reset failed");
+    }
+    *err = w.s1_err;
+    return BRD_OK;
+}
+
+// Reads (and clears) one of a slot's error words; the slot's stream is drained.
+static int take_err_word(Ctx::Slot &w, int *word, int *code) {
     *code = 0;
-    if (!w.s2_err) return BRD_OK;
-    HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, w.s2_err, sizeof(int), hipMemcpyDeviceToHost, w.s));
+    if (!word) return BRD_OK;
+    HIP_TRY(hipMemcpyAsync(g_ctx.s2_err_host, word, sizeof(int), hipMemcpyDeviceToHost, w.s));
     HIP_TRY(hipStreamSynchronize(w.s));
     *code = *g_ctx.s2_err_host;
     if (*code) {
-        HIP_TRY(hipMemsetAsync(w.s2_err, 0, sizeof(int), w.s));
+        HIP_TRY(hipMemsetAsync(word, 0, sizeof(int), w.s));
         HIP_TRY(hipStreamSynchronize(w.s));
     }
     return BRD_OK;
 }
+static int take_s2_error(Ctx::Slot &w, int *code) { return take_err_word(w, w.s2_err, code); }
+static int take_s1_error(Ctx::Slot &w, int *code) { return take_err_word(w, w.s1_err, code); }
 
 // HBM staging buffer of the host-pointer paths, cached per launch stream (no
 // allocation per call, nothing to free on an error return).
@@ -228,12 +246,16 @@ static int ensure_stage(size_t bytes, void **out) {
     return BRD_OK;
 }
 
-// Host-pointer calls stage the matrix in HBM; a staging buffer above this
-// size is freed when the call returns instead of being kept for the stream's
-// lifetime (2 GiB at 16384^2 fp64).
-static const size_t kStageKeep = (size_t)256 << 20;
+// Host-pointer calls stage the matrix in HBM.  The staging buffer is kept for
+// the stream's lifetime (brd_release_stream frees it): freeing it after every
+// call would make each call pay hipMalloc + hipFree, and hipFree synchronises
+// the whole device (other streams' work included).  BRD_STAGE_KEEP_MB caps
+// what is kept (a larger buffer is then freed when the call returns).
 static void trim_stage(Ctx::Slot &w) {
-    if (w.stage && w.stage_bytes > kStageKeep) {
+    static const char *kenv = getenv("BRD_STAGE_KEEP_MB");
+    if (!kenv) return;
+    const size_t keep = (size_t)std::max(0, atoi(kenv)) << 20;
+    if (w.stage && w.stage_bytes > keep) {
         hipStreamSynchronize(w.s);
         hipFree(w.stage);
         w.stage = nullptr;
@@ -463,8 +485,8 @@ static int ge2band_device(T *A, int m, int n, long lda, int b, hipStream_t s, bo
     if (rc) return rc;
     if (used_blocked) *used_blocked = kend > 0;
     if (kend > 0) {
-        int *prog = nullptr, *err = nullptr;
-        rc = ensure_s2_flags(n, &prog, &err);
+        int *err = nullptr;
+        rc = ensure_s1_err(&err);
         if (rc) return rc;
         HIP_TRY(blk_ge2band<T>(A, m, n, lda, wsbase, s, api_apply_target(), err));
     }
@@ -570,7 +592,7 @@ static int ge2band(T *A, int m, int n, int lda, int b, int ngpus, unsigned flags
         if (e != hipSuccess) return fail(BRD_EHIP, "stage 1: %s", hipGetErrorString(e));
         if (blocked && (!dev || !(flags & BRD_ASYNC))) {
             int code = 0;
-            rc = take_s2_error(slot(), &code);
+            rc = take_s1_error(slot(), &code);
             if (rc) return rc;
             if (code) return fail(BRD_EHIP, "stage 1: %s (code %d)", err_word_text(code), code);
         }
@@ -695,10 +717,12 @@ int brd_check_errors(void) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
     std::string bad;
     for (brd::Ctx::Slot &w : brd::g_ctx.slots) {
-        int code = 0;
-        const int rc = brd::take_s2_error(w, &code);
-        if (rc) return rc;
-        if (code) bad += (bad.empty() ? "" : ", ") + std::to_string(code);
+        for (int which = 0; which < 2; ++which) {
+            int code = 0;
+            const int rc = which ? brd::take_s1_error(w, &code) : brd::take_s2_error(w, &code);
+            if (rc) return rc;
+            if (code) bad += (bad.empty() ? "" : ", ") + std::to_string(code);
+        }
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return brd::fail(BRD_EHIP, "HIP error: %s", hipGetErrorString(e));
@@ -719,9 +743,11 @@ int brd_release_stream(void *hip_stream) {
         int code = 0;
         int h = 0;
         if (it->s2_err && hipMemcpy(&h, it->s2_err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) code = h;
+        if (!code && it->s1_err && hipMemcpy(&h, it->s1_err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) code = h;
         if (it->ws) hipFree(it->ws);
         if (it->s2_flags) hipFree(it->s2_flags);
         if (it->s2_err) hipFree(it->s2_err);
+        if (it->s1_err) hipFree(it->s1_err);
         if (it->stage) hipFree(it->stage);
         slots.erase(it);
         if (code)

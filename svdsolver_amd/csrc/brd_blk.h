@@ -1,0 +1,370 @@
+// Blocked stage 1 (dense -> band with a delayed two-sided update): shared
+// declarations of the kernels' translation units (brd_blk_rpass.hip,
+// brd_blk_prep.hip, brd_blk_cqr.hip, brd_blk_upd.hip) and the host drivers
+// (brd_stage1_blk.hip: one GPU; brd_dist.hip: the block-column-sharded
+// form).  See brd_stage1_blk.hip for the algorithm.
+#pragma once
+
+#include "brd_internal.h"
+
+#include <hip/hip_ext.h>
+
+#include <climits>
+
+namespace brd {
+namespace blk {
+
+// --------------------------------------------------------------------------
+// MFMA 16x16x4, one operand element per lane:
+//   A operand lane l: A[m = l&15][k = l>>4],  B operand lane l: B[k = l>>4][n = l&15]
+//   D register g of lane l: row crow(l>>4, g), column l&15
+// --------------------------------------------------------------------------
+template <typename T> struct Mf;
+template <> struct Mf<double> {
+    typedef double v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(double a, double b, v4 c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int crow(int q, int g) { return q + 4 * g; }
+};
+template <> struct Mf<float> {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(float a, float b, v4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int crow(int q, int g) { return 4 * q + g; }
+};
+
+template <typename T>
+struct G2 {   // two consecutive elements: 16 B (fp64) / 8 B (fp32)
+    typedef T v2 __attribute__((ext_vector_type(2)));
+};
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---- k_rpass (brd_blk_rpass.hip) ----------------------------------------------
+constexpr int NBMAX = 4;    // panels per block (Lw / RwT hold 2 NBMAX 32 = 256 vectors)
+constexpr int kRT = 512;    // threads: 4 column waves x 2 halves of the workgroup's K range
+constexpr int kWM = 64;     // m per wave
+constexpr int kMT = 256;    // m per workgroup
+#ifndef BRD_BLK_KSU
+#define BRD_BLK_KSU 8       // A/B knob (tools/variant_lib.sh)
+#endif
+constexpr int kSU = BRD_BLK_KSU;   // K steps in flight (Y); X: kSU / 2 step pairs
+
+constexpr int kRpLds = 8192;   // doubles
+struct RpArgs {
+    const void *src;  long ld;      // source S
+    const void *vsrc; long vld;     // virtual tile source (256 wide), or null
+    const void *bsrc; long bld;     // skinny operand B (k, t) = bsrc[k*bld + t]
+    int K, M;                       // S extents
+    int mtiles, ksplit, kper;       // kper: k per split (multiple of 8)
+    int nvirt;                      // ksplit if there is a virtual tile, else 0
+    void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
+    void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
+    void *vout;                     // virtual result [32][256] / [256][32]
+    int *counter;                   // (unused)
+    int *err;
+    int has_fin;                    // 1: workgroup 0 runs cqr_finish of the panel the pass follows
+};
+
+// ---- k_prep_* (brd_blk_prep.hip) ---------------------------------------------
+constexpr int kPT = 256;
+constexpr int kPI = 32;    // items per workgroup when split: two item waves x two halves of
+                           // the K1 range (the correction's MFMA chain over all four SIMDs;
+                           // the halves meet in LDS, fixed order); unsplit: 2 kPI items,
+                           // four item waves (when the split grid would exceed the CUs)
+
+struct PrepArgs {
+    void *A; long lda;
+    void *Lw; void *RwT; long ldr;
+    const void *part; long mp; int ksplit;
+    const void *G;            // virtual result of the read pass (LQ: [32][256], QR: [256][32])
+    const void *Tm;           // T_j (LQ) / S_{j-1} (QR), 32 x 32 row-major
+    void *Qp;                 // the corrected panel, transposed: QpT [32][mq] (both sides)
+    long mq;
+    int c;                    // panel column
+    int j;                    // panel index in the block
+    int items;
+    int reduce, factor;       // QR side switches
+    const double *sgn;        // s_t of the panel whose pass preceded (V' = Q was used: corrections)
+    int split;                // 1: kPI items, K1 in two halves; 0: 2 kPI items, one K range
+};
+
+constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
+constexpr int kLW = 226;
+constexpr int kQP = 40;    // QR pitch (rows k, k + 2 in opposite bank halves)
+
+// ---- k_cqr_* (brd_blk_cqr.hip) ----------------------------------------------
+constexpr int kCT = 256;
+constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
+constexpr int kCW = 64;   // most workgroups per panel (M <= kCW kCT rows)
+constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace ([32][kQS]: a lane per row, coalesced)
+
+struct CqrArgs {
+    const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
+    int M;
+    void *vdst; long vsi, vst;        // V(i, t)
+    void *vdst2; long vsi2, vst2;     // optional second copy of V (null: none)
+    void *tout;                       // T (32 x 32)
+    void *apan; long asi, ast;        // the panel in A: (i, t)
+    double *ws;                       // scratch (cqr_ws_doubles)
+    int *err;
+};
+
+// scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
+// per-workgroup exponents, R1, the shifted-pass flag, and Q1 [32][kCW kCT]
+__host__ __device__ constexpr size_t cqr_ws_doubles() {
+    return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
+}
+// Q_t (qt) and the zero flag are read by the next read pass's finishing
+// workgroup (cqr_finish)
+__host__ __device__ constexpr size_t cqr_ws_qt() { return (size_t)3 * 1024 * kCW + kCW + 1024; }
+__host__ __device__ constexpr size_t cqr_ws_zero() { return cqr_ws_qt() + 1024 + 2; }
+struct CqrWs {
+    double *gp1, *gp2, *ew, *r1, *qt, *shifted, *zero, *q1;
+    __device__ explicit CqrWs(double *ws)
+        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
+          qt(ws + cqr_ws_qt()), shifted(ws + cqr_ws_qt() + 1024), zero(ws + cqr_ws_zero()),
+          q1(ws + cqr_ws_zero() + 2) {}
+};
+
+struct CqrLds {
+    // the 32 x 32 matrices first: their LDS addresses fit the 16-bit offset field
+    double g[32][kSP];       // reduced Gram
+    double r1[32][kSP];      // R1 (upper, row-major)
+    double r2[32][kSP];      // R2
+    double u[32][kSP];       // U of the top block's LU (upper)
+    double mm[32][kSP];      // L^-1
+    double tq[32][kSP];      // Q's top block; then L (strict lower)
+    double r1w[32][kSP];     // R1 in trsm_row's form; then U^-1
+    double r2w[32][kSP];     // R2^-1 (first order) or R2 in trsm_row's form
+    double sgn[32];
+    double scl[kCW];         // per-partial scale factors of the Gram sum
+    int e_w;
+    int flags;
+    double q[4][64][33];     // per-wave staging of 64 rows (Gram, coalesced stores); per-wave Gram partials
+};
+
+__device__ __forceinline__ double rdl(double v, int l) {   // lane l's value, wave-uniform
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// Modified LU of Q_t - S = L U (Ballard et al. 2015: s_j = -sign of the
+// pivot, so every pivot has |.| >= 1) by one wave, lane r holding row r
+// (lanes 32-63 mirror).  The pivot row is lane jj's registers, broadcast by
+// readlanes (measured: 27 k clocks for the 32 steps; the same loop with the
+// pivot row published in LDS by its owner and read back as 16-byte
+// broadcasts took 34 k).  On return lane r's rv holds row r of L (strict
+// lower, unit diagonal implied) and U (upper); sgn[j] = s_j (LDS).
+__device__ __forceinline__ void lu_wave(double (&rv)[32], double *sgn, int lane) {
+    const int r = lane & 31;
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) {
+        double piv = rdl(rv[jj], jj);
+        const double sg = piv >= 0 ? -1.0 : 1.0;
+        piv -= sg;                                    // |piv| >= 1
+        double inv = __builtin_amdgcn_rcp(piv);
+        inv = fma(inv, fma(-piv, inv, 1.0), inv);
+        inv = fma(inv, fma(-piv, inv, 1.0), inv);
+        if (lane == 0) sgn[jj] = sg;
+        const bool below = r > jj;
+        const double l = rv[jj] * inv;
+        const double lb = below ? l : 0.0;   // rows <= jj: an exact no-op update, no selects
+#pragma unroll
+        for (int cc = jj + 1; cc < 32; ++cc) {
+            const double u = rdl(rv[cc], jj);
+            rv[cc] = fma(-lb, u, rv[cc]);
+            if (((cc - jj) & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bounds live scalar registers
+        }
+        rv[jj] = below ? l : (r == jj ? piv : rv[jj]);
+    }
+}
+
+// One 16 x 16 tile (ti, tj) of C = A B for 32 x 32 matrices in LDS, K range
+// [k0, 32) (k0 a multiple of 4: triangular operands skip their zero blocks).
+__device__ __forceinline__ Mf<double>::v4 tile_mm(const double (&A)[32][kSP], const double (&B)[32][kSP], int ti, int tj,
+                                                 int lane, int k0, int k1) {
+    const int q = lane >> 4, l15 = lane & 15;
+    Mf<double>::v4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = k0; k < k1; k += 4) acc = Mf<double>::mma(A[16 * ti + l15][k + q], B[k + q][16 * tj + l15], acc);
+    return acc;
+}
+__device__ __forceinline__ void tile_store(double (&C)[32][kSP], const Mf<double>::v4 &t, int ti, int tj, int lane) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) C[16 * ti + Mf<double>::crow(lane >> 4, g)][16 * tj + (lane & 15)] = t[g];
+}
+
+// --------------------------------------------------------------------------
+// cqr_finish: the rest of a panel's reconstruction, run by the first
+// workgroup of the read pass that follows the panel (k_rpass), beside the
+// pass itself -- the read pass uses V' = Q (the modified LU's signs enter
+// only V's top block, and Y_j = A^T V_j T_j is corrected by prep).  Wave 0:
+// the modified LU of Q_t - S = L U (s_j = -sign of the pivot); then wave 1
+// U^-1, wave 2 L^-1, wave 3 the band block R = S R' in place; then every
+// wave one tile of T = -S (U^-1 L^-1)^T.  A zero panel gets S = -I, T = 0.
+// All 512 threads of the workgroup pass the barriers; waves 4-7 idle.
+// --------------------------------------------------------------------------
+struct FinArgs {
+    const double *qt;     // Q_t (32 x 32, row-major)
+    const double *zero;   // 1: the panel was zero
+    double *sgn;          // out: s_j
+    void *tout;           // out: T
+    void *apan; long asi, ast;   // the band block R' (in place -> S R')
+};
+struct FinLds {
+    double u[32][kSP];       // U (upper)
+    double tq[32][kSP];      // Q_t, then L (strict lower)
+    double ui[32][kSP];      // U^-1
+    double li[32][kSP];      // L^-1
+    double sgn[32];
+};
+
+// (LDS matrices passed separately: k_cqr_v's inline use maps them onto its
+// own; tq_loaded: Q_t is already in tq)
+template <typename T>
+__device__ __forceinline__ void cqr_finish(double (&Lu)[32][kSP], double (&Ltq)[32][kSP], double (&Lui)[32][kSP],
+                                           double (&Lli)[32][kSP], double *Lsgn, const FinArgs &f, int tid,
+                                           bool tq_loaded) {
+    const int lane = tid & 63, w = tid >> 6;
+    const bool zero = f.zero[0] != 0.0;
+    if (!tq_loaded)
+        for (int el = tid; el < 1024; el += blockDim.x) Ltq[el >> 5][el & 31] = f.qt[el];
+    __syncthreads();
+    if (w == 0) {
+        const int r = lane & 31;
+        double rv[32];
+#pragma unroll
+        for (int cc = 0; cc < 32; ++cc) rv[cc] = Ltq[r][cc];
+        if (!zero) {
+            lu_wave(rv, Lsgn, lane);
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 32; ++jj) rv[jj] = r == jj ? 1.0 : 0.0;
+            if (lane < 32) Lsgn[lane] = -1.0;
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int cc = 0; cc < 32; ++cc) Lu[r][cc] = cc >= r ? rv[cc] : 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 32; ++cc) Ltq[r][cc] = cc < r ? rv[cc] : 0.0;
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+        if (lane < 32) f.sgn[lane] = Lsgn[lane];
+    } else if (w == 1) {
+        // U^-1 (lane c = column c, right-looking back substitution)
+        const int c = lane & 31;
+        double acc[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 31; k >= 0; --k) {
+            const double d = Lu[k][k];
+            double inv = __builtin_amdgcn_rcp(d);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            inv = fma(inv, fma(-d, inv, 1.0), inv);
+            const double xk = acc[k] * inv;
+            acc[k] = xk;
+#pragma unroll
+            for (int i2 = 0; i2 < k; ++i2) acc[i2] = fma(-Lu[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) Lui[k][c] = acc[k];
+        }
+    } else if (w == 2) {
+        // L^-1 (unit lower; lane c = column c, forward substitution)
+        const int c = lane & 31;
+        double acc[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const double xk = acc[k];
+#pragma unroll
+            for (int i2 = k + 1; i2 < 32; ++i2) acc[i2] = fma(-Ltq[i2][k], xk, acc[i2]);
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) Lli[k][c] = acc[k];
+        }
+    } else if (w == 3) {
+        // R = S R' (upper block, rows scaled by s_i)
+        T *ap = (T *)f.apan;
+        for (int el = lane; el < 1024; el += 64) {
+            const int i2 = el >> 5, c = el & 31;
+            if (i2 <= c) {
+                T *pp = ap + (size_t)i2 * f.asi + (size_t)c * f.ast;
+                *pp = (T)(Lsgn[i2] * (double)*pp);
+            }
+        }
+    }
+    __syncthreads();
+    if (w < 4) {
+        // T = -S (U^-1 L^-1)^T: wave w forms tile (w >> 1, w & 1) of U^-1 L^-1
+        const int ti = w >> 1, tj = w & 1;
+        const Mf<double>::v4 pt = tile_mm(Lui, Lli, ti, tj, lane, 16 * (ti > tj ? ti : tj), 32);
+        T *tout = (T *)f.tout;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), j2 = 16 * tj + (lane & 15);
+            tout[j2 * 32 + i2] = (T)(zero ? 0.0 : -Lsgn[j2] * pt[g]);
+        }
+    }
+}
+
+template <typename T>
+__device__ void cqr_finish_entry(const FinArgs &f, int tid, void *lds) {
+    static_assert(sizeof(FinLds) <= kRpLds * sizeof(double), "cqr_finish's LDS exceeds the read pass's block");
+    FinLds &FL = *reinterpret_cast<FinLds *>(lds);
+    cqr_finish<T>(FL.u, FL.tq, FL.ui, FL.li, FL.sgn, f, tid, false);
+}
+
+// ---- k_blkupd (brd_blk_upd.hip) ---------------------------------------------
+constexpr int kGT = 256;
+constexpr int kGM = 128;
+constexpr int kGKC = 16;
+constexpr int kGBP = kGM + 16;
+
+struct GemmArgs {
+    void *C; long ldc;
+    int rows, cols;                 // extent of the updated region
+    const void *Lw; const void *RwT; long ldr;
+    int K;                          // 256
+    int tiles_c;                    // column tiles
+    int ntiles;                     // tiles
+};
+
+// ---- launches ----------------------------------------------------------------
+// Every launch of the blocked path goes through blk_launch: with brd_profile
+// on, the launch itself stamps its start and end (hipExtLaunchKernel), tagged
+// with the kernel's algorithmic flops and HBM bytes (bench.py's roofline
+// objects).
+template <typename F, typename... Args>
+static inline void blk_launch(const char *kind, double flops, double bytes, F kernel, dim3 grid, dim3 block,
+                              hipStream_t s, Args... args) {
+    hipEvent_t ea, eb;
+    if (api_prof_launch_events(kind, flops, bytes, &ea, &eb))
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ea, eb, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
+
+// host launchers, one per kernel family, defined beside the kernels
+template <typename T>
+void launch_k_rpass(bool yp, dim3 grid, const RpArgs &a, const FinArgs &f, hipStream_t s, double fl, double by);
+template <typename T>
+void launch_k_vsum(const T *vpart, T *vout, int nvirt, T *pbase, long pstride, const double *sgn, hipStream_t s);
+template <typename T>
+void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s);
+enum CqrKernel { kCqrGram, kCqrQ1, kCqrV, kCqrVInline };
+template <typename T>
+void launch_k_cqr(CqrKernel which, int nwg, const CqrArgs &a, const FinArgs &f, hipStream_t s);
+template <typename T>
+void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, double by);
+
+}  // namespace blk
+}  // namespace brd

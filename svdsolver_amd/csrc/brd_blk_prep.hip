@@ -1,0 +1,430 @@
+// Blocked stage 1: the per-panel corrections k_prep_lq / k_prep_qr (gfx950).
+#include "brd_blk.h"
+
+namespace brd {
+namespace blk {
+
+// ==========================================================================
+// k_prep: the per-column (LQ side) / per-row (QR side) corrections, on the
+// matrix cores.  16 items per item wave; split (PrepArgs::split): 32 items per
+// workgroup, the K1 range in two halves (waves w and w + 2); else 64 items.
+//   LQ (item i = column c+32+i of panel j, c = panel column):
+//     y   = sum_ks part[ks][:][i] - sum_{k in K1} RwT[k][col] G[k][:]     K1 = V_<j, X_<j
+//     Y_j = y T_j                -> RwT[32j + t][col]
+//     q   = A[c+t][col] - sum_{k in K2} Lw[c+t][k] RwT[k][col]           K2 = V_<=j, X_<j
+//                                -> QpT[t][i]
+//     (computed transposed, D[t][i]: the B operand RwT[k][col0 + l15] is one
+//     coalesced load per lane and step, shared by both corrections)
+//   QR (item i = row c+i, c = column of panel j >= 1):
+//     x   = sum_ks part[ks][i][:] - sum_{k in K1} Lw[row][k] G[k][:]      K1 = V_<=j-1, X_<j-1
+//     X_{j-1} = x S_{j-1}        -> Lw[row][128 + 32(j-1) + t]
+//     factor: p = A[row][c+t] - sum_{k in K2} Lw[row][k] RwT[k][c+t]     K2 = V_<j, X_<j -> QpT[t][i]
+//     (D[i][t]: the A operand Lw[row][.] is read as 16-byte pairs, two k
+//     steps each, shared by both corrections)
+// K sets are kept compact in LDS: [0, 32a) and [128, 128 + 32b) stored
+// back to back.
+// ==========================================================================
+template <typename T>
+__global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
+    typedef typename Mf<T>::v4 v4;
+    __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
+    __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
+    __shared__ T Tt[32 * 34];    // T_j^T
+    __shared__ T Xh[2][16][64];  // the second K half's accumulators
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wi = a.split ? w & 1 : w, kh = a.split ? w >> 1 : 0;
+    const int q = lane >> 4, l15 = lane & 15;
+    const int j = a.j, c = a.c;
+    const int nk1 = 64 * j, nk2 = 64 * j + 32;
+    const T *G = (const T *)a.G;
+    const T *Lw = (const T *)a.Lw;
+    T *RwT = (T *)a.RwT;
+    // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
+    // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
+    // the operands first (their latency under the staging loads)
+    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * wi;
+    const int il = i0 + l15;                       // this lane's item (B operand / C column)
+    const bool iv = il < a.items;
+    const long col = (long)c + 32 + il;
+    const T *A = (const T *)a.A;
+    v4 ay[2], aq[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            ay[h][g] = (T)0;
+            aq[h][g] = (iv && kh == 0) ? A[(size_t)(c + t) * a.lda + col] : (T)0;
+        }
+    // ---- K1: both corrections share the B operand RwT[k][col] ----------------
+    // half kh = 0 takes the V_<j part (RwT rows [0, 32j)), kh = 1 the X_<j part
+    // (rows [128, 128 + 32j)); all B operands are loaded before the first MFMA
+    // (unconditional loads at clamped addresses, zeroed when out of range)
+    constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
+    const long colc = iv ? col : (long)c + 32;
+    T bk[2][kMS];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int s = 0; s < kMS; ++s) {
+            const int k1 = min(4 * s + q, max(32 * j - 1, 0)) + 128 * pp;
+            const bool mine = a.split ? pp == kh : true;
+            T v1 = (T)0;
+            if (mine) v1 = RwT[(size_t)k1 * a.ldr + colc];
+            bk[pp][s] = (iv && s < 8 * j) ? v1 : (T)0;
+        }
+    // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
+    if (tid < nk1) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
+    }
+    if (tid < nk2) {
+        const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
+    }
+    {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + kPT * u;
+            Tt[(e & 31) * 34 + (e >> 5)] = v[u];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        if (a.split && pp != kh) continue;
+        const int gb = pp ? 32 * j : 0, lb = pp ? 32 * j + 32 : 0;   // compact bases: V_<j | X_<j
+#pragma unroll
+        for (int s = 0; s < kMS; ++s) {
+            if (s < 8 * j) {
+                const int kk = 4 * s + q;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[pp][s], ay[h]);
+                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[pp][s], aq[h]);
+                }
+            }
+        }
+    }
+    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
+        if (kh) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    Xh[wi][4 * h + g][lane] = ay[h][g];
+                    Xh[wi][8 + 4 * h + g][lane] = aq[h][g];
+                }
+        }
+        __syncthreads();
+        if (kh) return;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                ay[h][g] += Xh[wi][4 * h + g][lane];
+                aq[h][g] += Xh[wi][8 + 4 * h + g][lane];
+            }
+    }
+    // ---- y = sum of split partials - correction ------------------------------
+    const T *part = (const T *)a.part;
+    T y[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) y[h][g] = (T)0;
+    const size_t ilc = iv ? il : 0;
+    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
+        T v[4][2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int t = 16 * h + Mf<T>::crow(q, g);
+                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * 32 + t) * a.mp + ilc];
+                }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if (k0 + u < a.ksplit) y[h][g] += v[u][h][g];
+    }
+    // the pass used V' = Q (top rows without -S): A_cur^T V = A_cur^T V' -
+    // A_cur[c:c+32, :]^T S, and aq here is exactly A_cur[c+t][col]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            y[h][g] = iv ? y[h][g] - ay[h][g] - (T)a.sgn[t] * aq[h][g] : (T)0;
+        }
+    // ---- Y_j^T = T_j^T y^T: the C registers of y are the B operand -----------
+    v4 ayj[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int u = 16 * hp + Mf<T>::crow(q, g);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) ayj[h] = Mf<T>::mma(Tt[(16 * h + l15) * 34 + u], y[hp][g], ayj[h]);
+        }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            if (iv) RwT[(size_t)(32 * j + t) * a.ldr + col] = ayj[h][g];
+        }
+    // ---- q += -Lw[c+t][32j + u] Y_j[u] ----------------------------------------
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int u = 16 * hp + Mf<T>::crow(q, g);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + 32 * j + u], ayj[hp][g], aq[h]);
+        }
+    T *QpT = (T *)a.Qp;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = 16 * h + Mf<T>::crow(q, g);
+            if (iv) QpT[(size_t)t * a.mq + il] = aq[h][g];
+        }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
+    typedef typename Mf<T>::v4 v4;
+    typedef typename G2<T>::v2 v2;
+    __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
+    __shared__ T Ss[32 * 48];        // S_{j-1}
+    __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
+    __shared__ T Xh[2][16][64];      // the second K half's accumulators
+    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
+    const int w = a.split ? wk & 1 : wk, kh = a.split ? wk >> 1 : 0;   // item wave, K half
+    const int q = lane >> 4, l15 = lane & 15;
+    const int j = a.j, jp = j - 1, c = a.c;
+    const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
+    const int n2 = a.factor ? 64 * j : 0;      // K2 compact: [0, 32j) | [128, 128 + 32j)
+    T *Rs = Gs + n1 * kQP;
+    const T *G = (const T *)a.G;
+    const T *RwT = (const T *)a.RwT;
+    T *Lw = (T *)a.Lw;
+    // the operands first (their latency under the staging loads)
+    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * w;
+    const int ia = i0 + l15;                        // A-operand row of this lane
+    const bool va = ia < a.items;
+    const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
+    const T *A = (const T *)a.A;
+    v4 ax[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}}, ap[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ic = i0 + Mf<T>::crow(q, g);
+            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
+        }
+    // ranges of Lw columns: [0, 32j) (compact 0; K half 0) and [128, 128 + 32jp)
+    // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
+    // (16-byte pairs of the lane's row) are loaded before the first MFMA.
+    constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
+    v2 av[2][kMP];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        const int ng = pp ? 4 * jp : 4 * j;
+        const bool mine = a.split ? pp == kh : true;
+#pragma unroll
+        for (int s = 0; s < kMP; ++s) {
+            const int kl = min(8 * s, max(8 * ng - 8, 0)) + 2 * q + 128 * pp;
+            v2 u = v2{(T)0, (T)0};
+            if (mine) u = *(const v2 *)(lrow + kl);
+            av[pp][s] = (va && s < ng) ? u : v2{(T)0, (T)0};
+        }
+    }
+    // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
+    if (tid < n1) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)k * 32 + t];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Gs[kk * kQP + t] = v[t];
+    }
+    if (tid < n2) {
+        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
+        T v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + c + t];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) Rs[kk * kQP + t] = -v[t];
+    }
+    {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + kPT * u;
+            Ss[(e >> 5) * 48 + (e & 31)] = v[u];
+        }
+    }
+    __syncthreads();
+
+    auto krange = [&](const v2 (&av)[kMP], int cb, int ngrp) {
+#pragma unroll
+        for (int s = 0; s < kMP; ++s) {
+            if (s < ngrp) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int kk = cb + 8 * s + 2 * q + e;
+                    const T x = e ? av[s].y : av[s].x;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        ax[h] = Mf<T>::mma(x, Gs[kk * kQP + 16 * h + l15], ax[h]);
+                        if (a.factor) ap[h] = Mf<T>::mma(x, Rs[kk * kQP + 16 * h + l15], ap[h]);
+                    }
+                }
+            }
+        }
+    };
+    if (!a.split || kh == 0) krange(av[0], 0, 4 * j);         // V_<j      (K1 and K2)
+    if (!a.split || kh == 1) krange(av[1], 32 * j, 4 * jp);   // X_<j-1    (K1 and K2)
+    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
+        if (kh) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    Xh[w][4 * h + g][lane] = ax[h][g];
+                    Xh[w][8 + 4 * h + g][lane] = ap[h][g];
+                }
+        }
+        __syncthreads();
+        if (kh) return;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                ax[h][g] += Xh[w][4 * h + g][lane];
+                ap[h][g] += Xh[w][8 + 4 * h + g][lane];
+            }
+    }
+    // ---- x = sum of split partials - correction; X_{j-1} = x S ---------------
+    const T *part = (const T *)a.part;
+    T xs[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xs[h][g] = (T)0;
+    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
+        T v[4][2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int ic = min(i0 + Mf<T>::crow(q, g), a.items - 1), t = 16 * h + l15;
+                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * a.mp + ic) * 32 + t];
+                }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if (k0 + u < a.ksplit) xs[h][g] += v[u][h][g];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = Mf<T>::crow(q, g), t = 16 * h + l15;
+            // the pass used U' = Q: ap here is A_cur[row][c + t] (corrections;
+            // the block end's reduce-only call follows an inline finish: none)
+            const T corr = a.factor ? (T)a.sgn[t] * ap[h][g] : (T)0;
+            Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] - corr : (T)0;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    v4 xx[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int u = 4 * s + q;
+        const T av = Tb[w][l15 * 34 + u];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) xx[h] = Mf<T>::mma(av, Ss[u * 48 + 16 * h + l15], xx[h]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = Mf<T>::crow(q, g), ic = i0 + r, t = 16 * h + l15;
+            if (ic < a.items) Lw[(size_t)(c + ic) * 256 + 128 + 32 * jp + t] = xx[h][g];
+            Tb[w][r * 34 + t] = xx[h][g];
+        }
+    if (!a.factor) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- p += -X_{j-1}[row][u] RwT[128 + 32jp + u][c+t] -----------------------
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int u = 4 * s + q;
+        const T av = Tb[w][l15 * 34 + u];
+        const int kk = 32 * j + 32 * jp + u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ap[h] = Mf<T>::mma(av, Rs[kk * kQP + 16 * h + l15], ap[h]);
+    }
+    // P^T [32][mq] (the panel QR reads a lane per row: coalesced), through the
+    // wave's transpose tile: 16 consecutive items x 4 t per store
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Tb[w][Mf<T>::crow(q, g) * 34 + 16 * h + l15] = ap[h][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    T *QpT = (T *)a.Qp;
+    const bool vs = i0 + l15 < a.items;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int t = 4 * it + q;
+        if (vs) QpT[(size_t)t * a.mq + i0 + l15] = Tb[w][l15 * 34 + t];
+    }
+}
+
+template <typename T>
+void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s) {
+    if (lq) blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, grid, dim3(kPT), s, p);
+    else    blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, grid, dim3(kPT), s, p);
+}
+template void launch_k_prep<double>(bool, dim3, const PrepArgs &, hipStream_t);
+template void launch_k_prep<float>(bool, dim3, const PrepArgs &, hipStream_t);
+
+}  // namespace blk
+}  // namespace brd

@@ -62,8 +62,9 @@ hipError_t launch_apply(bool trans, T *base, long ld, const Tree &t, int level,
 // Blocked stage 1 (brd_stage1_blk.hip): panels of width 32 grouped in blocks
 // of 4 with a delayed two-sided update.  blk_columns: columns [0, kend) the
 // blocked path reduces (0 when it does not apply); the caller finishes the
-// remaining panels with the per-panel path.  err: device error word (2:
-// cluster barrier timeout, 3: CholeskyQR breakdown).
+// remaining panels with the per-panel path.  err: the stage-1 device error
+// word (3: CholeskyQR breakdown -- a non-finite panel; rank deficiency is
+// handled, cqr_shifted_pass).
 size_t blk_ws_bytes(int m, int n, size_t elem);
 int blk_columns(int m, int n, int b);
 template <typename T>

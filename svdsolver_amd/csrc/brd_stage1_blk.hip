@@ -23,1644 +23,16 @@
 //
 // The executable specification (same steps, same workspaces) is
 // tests/s1_model.py; DESIGN.md "Stage 1, blocked" has the roofline of each
-// kernel.
-#include "brd_internal.h"
-
-#include <hip/hip_ext.h>
+// kernel.  This file is the host driver; the kernels live in brd_blk_*.hip
+// (brd_blk.h).
+#include "brd_blk.h"
 
 #include <algorithm>
-#include <climits>
-#include <cstdlib>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace brd {
-namespace blk {
-
-// --------------------------------------------------------------------------
-// MFMA 16x16x4, one operand element per lane:
-//   A operand lane l: A[m = l&15][k = l>>4],  B operand lane l: B[k = l>>4][n = l&15]
-//   D register g of lane l: row crow(l>>4, g), column l&15
-// --------------------------------------------------------------------------
-template <typename T> struct Mf;
-template <> struct Mf<double> {
-    typedef double v4 __attribute__((ext_vector_type(4)));
-    static __device__ __forceinline__ v4 mma(double a, double b, v4 c) {
-        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ int crow(int q, int g) { return q + 4 * g; }
-};
-template <> struct Mf<float> {
-    typedef float v4 __attribute__((ext_vector_type(4)));
-    static __device__ __forceinline__ v4 mma(float a, float b, v4 c) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ int crow(int q, int g) { return 4 * q + g; }
-};
-
-template <typename T>
-struct G2 {   // two consecutive elements: 16 B (fp64) / 8 B (fp32)
-    typedef T v2 __attribute__((ext_vector_type(2)));
-};
-
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// ==========================================================================
-// k_rpass: D = B^T S (Y pass) or S B (X pass) for a tall "skinny" operand B
-// (K x 32) and a source S, summed over one split of the K range.
-//   Y pass (YP): S(k, m) = src[k*ld + m] (row-major A, k = rows, m = columns),
-//                D[t][m] = sum_k B[k][t] S(k, m); partials stored [split][t][m].
-//   X pass     : S(k, m) = src[m*ld + k] (k = columns, m = rows),
-//                D[m][t] = sum_k S(k, m) B[k][t]; partials stored [split][m][t].
-// B(k, t) = bsrc[k*bld + t] in both.  Every wave streams its own 64 values of
-// m straight from HBM into MFMA operand registers (no LDS, no barriers):
-//   Y: one 16-byte load per lane and 4 rows gives 2 x 16 columns (even / odd
-//      column tiles), 4 rows x 256 contiguous bytes per instruction;
-//   X: one 16-byte load per lane gives 2 k of one row: 16 rows x 64 bytes per
-//      instruction, two K steps each;
-// with kSU steps of loads in flight (static register ring).  The "virtual"
-// workgroups (the first ksplit of the grid) compute the same product with
-// S = vsrc (256 wide); they meet at a counter and each sums one slice of
-// their partials into vout in fixed order (deterministic).
-// ==========================================================================
-constexpr int NBMAX = 4;    // panels per block (Lw / RwT hold 2 NBMAX 32 = 256 vectors)
-constexpr int kRT = 512;    // threads: 4 column waves x 2 halves of the workgroup's K range
-constexpr int kWM = 64;     // m per wave
-constexpr int kMT = 256;    // m per workgroup
-#ifndef BRD_BLK_KSU
-#define BRD_BLK_KSU 8       // A/B knob (tools/variant_lib.sh)
-#endif
-constexpr int kSU = BRD_BLK_KSU;   // K steps in flight (Y); X: kSU / 2 step pairs
-
-constexpr int kRpLds = 8192;   // doubles
-struct RpArgs {
-    const void *src;  long ld;      // source S
-    const void *vsrc; long vld;     // virtual tile source (256 wide), or null
-    const void *bsrc; long bld;     // skinny operand B (k, t) = bsrc[k*bld + t]
-    int K, M;                       // S extents
-    int mtiles, ksplit, kper;       // kper: k per split (multiple of 8)
-    int nvirt;                      // ksplit if there is a virtual tile, else 0
-    void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
-    void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
-    void *vout;                     // virtual result [32][256] / [256][32]
-    int *counter;                   // (unused)
-    int *err;
-    int has_fin;                    // 1: workgroup 0 runs cqr_finish of the panel the pass follows
-};
-
-struct FinArgs;
-template <typename T>
-__device__ void cqr_finish_entry(const FinArgs &f, int tid, void *lds);
-
-template <typename T, bool YP, typename FA>
-__global__ void __launch_bounds__(kRT, 1) k_rpass(RpArgs a, FA fin) {
-    typedef typename G2<T>::v2 v2;
-    typedef typename Mf<T>::v4 v4;
-    const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, kh = tid >> 8;
-    const int q = lane >> 4, l15 = lane & 15;
-    // one LDS block for the K halves' reduction and (workgroup 0) cqr_finish:
-    // 64 KB, so two workgroups share a CU
-    __shared__ __attribute__((aligned(16))) double rp_lds[kRpLds];
-    if (a.has_fin && blockIdx.x == 0) {   // the previous panel's LU, T and R signs, beside the pass
-        cqr_finish_entry<T>(fin, tid, rp_lds);
-        return;
-    }
-    const int bid = blockIdx.x - a.has_fin;
-    const bool virt = bid < a.nvirt;
-    int mx, ks;
-    if (virt) { mx = 0; ks = bid; }
-    else      { const int r = bid - a.nvirt; mx = r % a.mtiles; ks = r / a.mtiles; }
-    const T *S;
-    long ld;
-    int M;
-    if (virt) { S = (const T *)a.vsrc; ld = a.vld; M = kMT; }
-    else      { S = (const T *)a.src + (YP ? (long)mx * kMT : (long)mx * kMT * a.ld); ld = a.ld; M = min(kMT, a.M - mx * kMT); }
-    const T *B = (const T *)a.bsrc;
-    // waves w and w + 4 take the two halves of the workgroup's K range (in
-    // whole 8-row step pairs) and meet in LDS: two waves per SIMD in flight
-    const int kb0 = ks * a.kper, ke0 = min(a.K, kb0 + a.kper);
-    const int khalf = ke0 > kb0 ? ((ke0 - kb0 + 15) / 16) * 8 : 0;
-    const int kbeg = kh ? min(ke0, kb0 + khalf) : kb0, kend = kh ? ke0 : min(ke0, kb0 + khalf);
-    const int mb = kWM * w;
-    v4 acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = v4{0, 0, 0, 0};
-
-    if constexpr (YP) {
-        // acc[h*4 + p*2 + e]: t-half h, column pair group p (32 columns), parity e
-        const int nst = kend > kbeg ? (kend - kbeg + 3) / 4 : 0;
-        v2 ra[kSU][2];
-        T rb[kSU][2];
-        auto load = [&](int s, v2 (&va)[2], T (&vb)[2]) {
-            const int k = kbeg + 4 * s + q;
-            const bool kv = k < kend;
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int m = mb + 32 * p + 2 * l15;
-                v2 v = {(T)0, (T)0};
-                if (kv && m < M) {
-                    const T *src = S + (long)k * ld + m;
-                    if (m + 1 < M) v = *(const v2 *)src; else v.x = src[0];
-                }
-                va[p] = v;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) vb[h] = kv ? B[(long)k * a.bld + 16 * h + l15] : (T)0;
-        };
-#pragma unroll
-        for (int u = 0; u < kSU; ++u)
-            if (u < nst) load(u, ra[u], rb[u]);
-        for (int s0 = 0; s0 < nst; s0 += kSU) {
-#pragma unroll
-            for (int u = 0; u < kSU; ++u) {
-                const int s = s0 + u;
-                if (s < nst) {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int p = 0; p < 2; ++p) {
-                            acc[h * 4 + p * 2 + 0] = Mf<T>::mma(rb[u][h], ra[u][p].x, acc[h * 4 + p * 2 + 0]);
-                            acc[h * 4 + p * 2 + 1] = Mf<T>::mma(rb[u][h], ra[u][p].y, acc[h * 4 + p * 2 + 1]);
-                        }
-                    if (s + kSU < nst) load(s + kSU, ra[u], rb[u]);
-                }
-            }
-        }
-    } else {
-        // acc[p*2 + h]: row tile p (16 rows), t-half h; one step pair = 8 k
-        const int npr = kend > kbeg ? (kend - kbeg + 7) / 8 : 0;
-        constexpr int kSP2 = kSU / 2;
-        v2 ra[kSP2][4];
-        T rb[kSP2][2][2];
-        auto load = [&](int s2, v2 (&va)[4], T (&vb)[2][2]) {
-            const int k = kbeg + 8 * s2 + 2 * q;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int m = mb + 16 * p + l15;
-                v2 v = {(T)0, (T)0};
-                if (m < M && k < kend) {
-                    const T *src = S + (long)m * ld + k;
-                    if (k + 1 < kend) v = *(const v2 *)src; else v.x = src[0];
-                }
-                va[p] = v;
-            }
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) vb[e][h] = (k + e < kend) ? B[(long)(k + e) * a.bld + 16 * h + l15] : (T)0;
-        };
-#pragma unroll
-        for (int u = 0; u < kSP2; ++u)
-            if (u < npr) load(u, ra[u], rb[u]);
-        for (int s0 = 0; s0 < npr; s0 += kSP2) {
-#pragma unroll
-            for (int u = 0; u < kSP2; ++u) {
-                const int s2 = s0 + u;
-                if (s2 < npr) {
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            acc[p * 2 + h] = Mf<T>::mma(ra[u][p].x, rb[u][0][h], acc[p * 2 + h]);
-                            acc[p * 2 + h] = Mf<T>::mma(ra[u][p].y, rb[u][1][h], acc[p * 2 + h]);
-                        }
-                    if (s2 + kSP2 < npr) load(s2 + kSP2, ra[u], rb[u]);
-                }
-            }
-        }
-    }
-
-    // ---- the second half's sums into the first half's, fixed order ----------
-    {
-        T (*red)[32][64] = reinterpret_cast<T (*)[32][64]>(rp_lds);
-        if (kh) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) red[w][4 * i + g][lane] = acc[i][g];
-        }
-        __syncthreads();
-        if (!kh) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) acc[i][g] += red[w][4 * i + g][lane];
-        }
-    }
-    // ---- partials ----------------------------------------------------------
-    T *out;
-    long mp;
-    if (virt) { out = (T *)a.vpart + (size_t)ks * 32 * kMT; mp = kMT; }
-    else      { out = (T *)a.part + (size_t)ks * 32 * a.mp + (size_t)mx * kMT * (YP ? 1 : 32); mp = a.mp; }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (kh) break;
-            const int r = Mf<T>::crow(q, g);
-            if (YP) {
-                const int h = i >> 2, p = (i >> 1) & 1, e = i & 1;
-                const int t = 16 * h + r, m = mb + 32 * p + 2 * l15 + e;
-                if (m < M) out[(size_t)t * mp + m] = acc[i][g];
-            } else {
-                const int p = i >> 1, h = i & 1;
-                const int m = mb + 16 * p + r, t = 16 * h + l15;
-                if (m < M) out[(size_t)m * 32 + t] = acc[i][g];
-            }
-        }
-}
-
-// The virtual tile's split-K partials summed in fixed order (one element per
-// thread, every partial's load in flight at once): a kernel of its own, so
-// no workgroup of the read pass waits for another.
-// Workgroup 0 also patches the diagonal of the finished panel's top block
-// from V' = Q to V = Q - S (pbase[t (pstride)] -= s_t), read from here on.
-template <typename T>
-__global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt, T *pbase, long pstride,
-                                              const double *sgn) {
-    const int e = blockIdx.x * 256 + threadIdx.x;   // < 32 kMT
-    if (blockIdx.x == 0 && threadIdx.x < 32 && pbase)
-        pbase[(size_t)threadIdx.x * pstride] = (T)((double)pbase[(size_t)threadIdx.x * pstride] - sgn[threadIdx.x]);
-    T v[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) v[k] = vpart[(size_t)min(k, nvirt - 1) * 32 * kMT + e];
-    T s = v[0];
-#pragma unroll
-    for (int k = 1; k < 32; ++k)
-        if (k < nvirt) s += v[k];
-    vout[e] = s;
-}
-
-// ==========================================================================
-// k_prep: the per-column (LQ side) / per-row (QR side) corrections, on the
-// matrix cores.  16 items per item wave; split (PrepArgs::split): 32 items per
-// workgroup, the K1 range in two halves (waves w and w + 2); else 64 items.
-//   LQ (item i = column c+32+i of panel j, c = panel column):
-//     y   = sum_ks part[ks][:][i] - sum_{k in K1} RwT[k][col] G[k][:]     K1 = V_<j, X_<j
-//     Y_j = y T_j                -> RwT[32j + t][col]
-//     q   = A[c+t][col] - sum_{k in K2} Lw[c+t][k] RwT[k][col]           K2 = V_<=j, X_<j
-//                                -> QpT[t][i]
-//     (computed transposed, D[t][i]: the B operand RwT[k][col0 + l15] is one
-//     coalesced load per lane and step, shared by both corrections)
-//   QR (item i = row c+i, c = column of panel j >= 1):
-//     x   = sum_ks part[ks][i][:] - sum_{k in K1} Lw[row][k] G[k][:]      K1 = V_<=j-1, X_<j-1
-//     X_{j-1} = x S_{j-1}        -> Lw[row][128 + 32(j-1) + t]
-//     factor: p = A[row][c+t] - sum_{k in K2} Lw[row][k] RwT[k][c+t]     K2 = V_<j, X_<j -> QpT[t][i]
-//     (D[i][t]: the A operand Lw[row][.] is read as 16-byte pairs, two k
-//     steps each, shared by both corrections)
-// K sets are kept compact in LDS: [0, 32a) and [128, 128 + 32b) stored
-// back to back.
-// ==========================================================================
-constexpr int kPT = 256;
-constexpr int kPI = 32;    // items per workgroup when split: two item waves x two halves of
-                           // the K1 range (the correction's MFMA chain over all four SIMDs;
-                           // the halves meet in LDS, fixed order); unsplit: 2 kPI items,
-                           // four item waves (when the split grid would exceed the CUs)
-
-struct PrepArgs {
-    void *A; long lda;
-    void *Lw; void *RwT; long ldr;
-    const void *part; long mp; int ksplit;
-    const void *G;            // virtual result of the read pass (LQ: [32][256], QR: [256][32])
-    const void *Tm;           // T_j (LQ) / S_{j-1} (QR), 32 x 32 row-major
-    void *Qp;                 // the corrected panel, transposed: QpT [32][mq] (both sides)
-    long mq;
-    int c;                    // panel column
-    int j;                    // panel index in the block
-    int items;
-    int reduce, factor;       // QR side switches
-    const double *sgn;        // s_t of the panel whose pass preceded (V' = Q was used: corrections)
-    int split;                // 1: kPI items, K1 in two halves; 0: 2 kPI items, one K range
-};
-
-constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
-constexpr int kLW = 226;
-constexpr int kQP = 40;    // QR pitch (rows k, k + 2 in opposite bank halves)
-
-template <typename T>
-__global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
-#if BRD_DIAG_PREP == 1
-    return;
-#endif
-    typedef typename Mf<T>::v4 v4;
-    __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
-    __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
-    __shared__ T Tt[32 * 34];    // T_j^T
-    __shared__ T Xh[2][16][64];  // the second K half's accumulators
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wi = a.split ? w & 1 : w, kh = a.split ? w >> 1 : 0;
-    const int q = lane >> 4, l15 = lane & 15;
-    const int j = a.j, c = a.c;
-    const int nk1 = 64 * j, nk2 = 64 * j + 32;
-    const T *G = (const T *)a.G;
-    const T *Lw = (const T *)a.Lw;
-    T *RwT = (T *)a.RwT;
-    // K1 compact index kk -> k: kk < 32j: kk; else 128 + kk - 32j.
-    // K2 compact: kk < 32(j+1): kk; else 128 + kk - 32(j+1).
-    // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * wi;
-    const int il = i0 + l15;                       // this lane's item (B operand / C column)
-    const bool iv = il < a.items;
-    const long col = (long)c + 32 + il;
-    const T *A = (const T *)a.A;
-    v4 ay[2], aq[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int t = 16 * h + Mf<T>::crow(q, g);
-            ay[h][g] = (T)0;
-            aq[h][g] = (iv && kh == 0) ? A[(size_t)(c + t) * a.lda + col] : (T)0;
-        }
-    // ---- K1: both corrections share the B operand RwT[k][col] ----------------
-    // half kh = 0 takes the V_<j part (RwT rows [0, 32j)), kh = 1 the X_<j part
-    // (rows [128, 128 + 32j)); all B operands are loaded before the first MFMA
-    // (unconditional loads at clamped addresses, zeroed when out of range)
-    constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
-    const long colc = iv ? col : (long)c + 32;
-    T bk[2][kMS];
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp)
-#pragma unroll
-        for (int s = 0; s < kMS; ++s) {
-            const int k1 = min(4 * s + q, max(32 * j - 1, 0)) + 128 * pp;
-            const bool mine = a.split ? pp == kh : true;
-            T v1 = (T)0;
-            if (mine) v1 = RwT[(size_t)k1 * a.ldr + colc];
-            bk[pp][s] = (iv && s < 8 * j) ? v1 : (T)0;
-        }
-    // staging: thread -> compact column kk (< 256 threads), 32 independent loads each
-    if (tid < nk1) {
-        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
-    }
-    if (tid < nk2) {
-        const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
-    }
-    {
-        T v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = tid + kPT * u;
-            Tt[(e & 31) * 34 + (e >> 5)] = v[u];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-        if (a.split && pp != kh) continue;
-        const int gb = pp ? 32 * j : 0, lb = pp ? 32 * j + 32 : 0;   // compact bases: V_<j | X_<j
-#pragma unroll
-        for (int s = 0; s < kMS; ++s) {
-            if (s < 8 * j) {
-                const int kk = 4 * s + q;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[pp][s], ay[h]);
-                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[pp][s], aq[h]);
-                }
-            }
-        }
-    }
-    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
-        if (kh) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    Xh[wi][4 * h + g][lane] = ay[h][g];
-                    Xh[wi][8 + 4 * h + g][lane] = aq[h][g];
-                }
-        }
-        __syncthreads();
-        if (kh) return;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                ay[h][g] += Xh[wi][4 * h + g][lane];
-                aq[h][g] += Xh[wi][8 + 4 * h + g][lane];
-            }
-    }
-    // ---- y = sum of split partials - correction ------------------------------
-    const T *part = (const T *)a.part;
-    T y[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) y[h][g] = (T)0;
-    const size_t ilc = iv ? il : 0;
-    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
-        T v[4][2][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int t = 16 * h + Mf<T>::crow(q, g);
-                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * 32 + t) * a.mp + ilc];
-                }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    if (k0 + u < a.ksplit) y[h][g] += v[u][h][g];
-    }
-    // the pass used V' = Q (top rows without -S): A_cur^T V = A_cur^T V' -
-    // A_cur[c:c+32, :]^T S, and aq here is exactly A_cur[c+t][col]
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int t = 16 * h + Mf<T>::crow(q, g);
-            y[h][g] = iv ? y[h][g] - ay[h][g] - (T)a.sgn[t] * aq[h][g] : (T)0;
-        }
-    // ---- Y_j^T = T_j^T y^T: the C registers of y are the B operand -----------
-    v4 ayj[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
-#pragma unroll
-    for (int hp = 0; hp < 2; ++hp)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int u = 16 * hp + Mf<T>::crow(q, g);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) ayj[h] = Mf<T>::mma(Tt[(16 * h + l15) * 34 + u], y[hp][g], ayj[h]);
-        }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int t = 16 * h + Mf<T>::crow(q, g);
-            if (iv) RwT[(size_t)(32 * j + t) * a.ldr + col] = ayj[h][g];
-        }
-    // ---- q += -Lw[c+t][32j + u] Y_j[u] ----------------------------------------
-#pragma unroll
-    for (int hp = 0; hp < 2; ++hp)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int u = 16 * hp + Mf<T>::crow(q, g);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + 32 * j + u], ayj[hp][g], aq[h]);
-        }
-    T *QpT = (T *)a.Qp;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int t = 16 * h + Mf<T>::crow(q, g);
-            if (iv) QpT[(size_t)t * a.mq + il] = aq[h][g];
-        }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
-#if BRD_DIAG_PREP == 1
-    return;
-#endif
-    typedef typename Mf<T>::v4 v4;
-    typedef typename G2<T>::v2 v2;
-    __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
-    __shared__ T Ss[32 * 48];        // S_{j-1}
-    __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
-    __shared__ T Xh[2][16][64];      // the second K half's accumulators
-    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
-    const int w = a.split ? wk & 1 : wk, kh = a.split ? wk >> 1 : 0;   // item wave, K half
-    const int q = lane >> 4, l15 = lane & 15;
-    const int j = a.j, jp = j - 1, c = a.c;
-    const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
-    const int n2 = a.factor ? 64 * j : 0;      // K2 compact: [0, 32j) | [128, 128 + 32j)
-    T *Rs = Gs + n1 * kQP;
-    const T *G = (const T *)a.G;
-    const T *RwT = (const T *)a.RwT;
-    T *Lw = (T *)a.Lw;
-    // the operands first (their latency under the staging loads)
-    const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * w;
-    const int ia = i0 + l15;                        // A-operand row of this lane
-    const bool va = ia < a.items;
-    const T *lrow = Lw + (size_t)(c + (va ? ia : 0)) * 256;
-    const T *A = (const T *)a.A;
-    v4 ax[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}}, ap[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int ic = i0 + Mf<T>::crow(q, g);
-            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
-        }
-    // ranges of Lw columns: [0, 32j) (compact 0; K half 0) and [128, 128 + 32jp)
-    // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
-    // (16-byte pairs of the lane's row) are loaded before the first MFMA.
-    constexpr int kMP = 4 * NBMAX;   // most 8-column groups per range
-    v2 av[2][kMP];
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-        const int ng = pp ? 4 * jp : 4 * j;
-        const bool mine = a.split ? pp == kh : true;
-#pragma unroll
-        for (int s = 0; s < kMP; ++s) {
-            const int kl = min(8 * s, max(8 * ng - 8, 0)) + 2 * q + 128 * pp;
-            v2 u = v2{(T)0, (T)0};
-            if (mine) u = *(const v2 *)(lrow + kl);
-            av[pp][s] = (va && s < ng) ? u : v2{(T)0, (T)0};
-        }
-    }
-    // staging: thread -> compact row kk (< 256 threads), 32 independent loads each
-    if (tid < n1) {
-        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = G[(size_t)k * 32 + t];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Gs[kk * kQP + t] = v[t];
-    }
-    if (tid < n2) {
-        const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
-        T v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + c + t];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) Rs[kk * kQP + t] = -v[t];
-    }
-    {
-        T v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ((const T *)a.Tm)[tid + kPT * u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = tid + kPT * u;
-            Ss[(e >> 5) * 48 + (e & 31)] = v[u];
-        }
-    }
-    __syncthreads();
-#if BRD_DIAG_PREP == 2
-    return;
-#endif
-
-    auto krange = [&](const v2 (&av)[kMP], int cb, int ngrp) {
-#pragma unroll
-        for (int s = 0; s < kMP; ++s) {
-            if (s < ngrp) {
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int kk = cb + 8 * s + 2 * q + e;
-                    const T x = e ? av[s].y : av[s].x;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        ax[h] = Mf<T>::mma(x, Gs[kk * kQP + 16 * h + l15], ax[h]);
-                        if (a.factor) ap[h] = Mf<T>::mma(x, Rs[kk * kQP + 16 * h + l15], ap[h]);
-                    }
-                }
-            }
-        }
-    };
-    if (!a.split || kh == 0) krange(av[0], 0, 4 * j);         // V_<j      (K1 and K2)
-    if (!a.split || kh == 1) krange(av[1], 32 * j, 4 * jp);   // X_<j-1    (K1 and K2)
-    if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
-        if (kh) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    Xh[w][4 * h + g][lane] = ax[h][g];
-                    Xh[w][8 + 4 * h + g][lane] = ap[h][g];
-                }
-        }
-        __syncthreads();
-        if (kh) return;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                ax[h][g] += Xh[w][4 * h + g][lane];
-                ap[h][g] += Xh[w][8 + 4 * h + g][lane];
-            }
-    }
-    // ---- x = sum of split partials - correction; X_{j-1} = x S ---------------
-    const T *part = (const T *)a.part;
-    T xs[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) xs[h][g] = (T)0;
-    for (int k0 = 0; k0 < a.ksplit; k0 += 4) {
-        T v[4][2][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int ic = min(i0 + Mf<T>::crow(q, g), a.items - 1), t = 16 * h + l15;
-                    v[u][h][g] = part[((size_t)min(k0 + u, a.ksplit - 1) * a.mp + ic) * 32 + t];
-                }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    if (k0 + u < a.ksplit) xs[h][g] += v[u][h][g];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int r = Mf<T>::crow(q, g), t = 16 * h + l15;
-            // the pass used U' = Q: ap here is A_cur[row][c + t] (corrections;
-            // the block end's reduce-only call follows an inline finish: none)
-            const T corr = a.factor ? (T)a.sgn[t] * ap[h][g] : (T)0;
-            Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] - corr : (T)0;
-        }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    v4 xx[2] = {v4{0, 0, 0, 0}, v4{0, 0, 0, 0}};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const int u = 4 * s + q;
-        const T av = Tb[w][l15 * 34 + u];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) xx[h] = Mf<T>::mma(av, Ss[u * 48 + 16 * h + l15], xx[h]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int r = Mf<T>::crow(q, g), ic = i0 + r, t = 16 * h + l15;
-            if (ic < a.items) Lw[(size_t)(c + ic) * 256 + 128 + 32 * jp + t] = xx[h][g];
-            Tb[w][r * 34 + t] = xx[h][g];
-        }
-    if (!a.factor) return;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- p += -X_{j-1}[row][u] RwT[128 + 32jp + u][c+t] -----------------------
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const int u = 4 * s + q;
-        const T av = Tb[w][l15 * 34 + u];
-        const int kk = 32 * j + 32 * jp + u;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) ap[h] = Mf<T>::mma(av, Rs[kk * kQP + 16 * h + l15], ap[h]);
-    }
-    // P^T [32][mq] (the panel QR reads a lane per row: coalesced), through the
-    // wave's transpose tile: 16 consecutive items x 4 t per store
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) Tb[w][Mf<T>::crow(q, g) * 34 + 16 * h + l15] = ap[h][g];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    T *QpT = (T *)a.Qp;
-    const bool vs = i0 + l15 < a.items;
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int t = 4 * it + q;
-        if (vs) QpT[(size_t)t * a.mq + i0 + l15] = Tb[w][l15 * 34 + t];
-    }
-}
-
-// ==========================================================================
-// k_cqr_*: QR of a tall M x 32 panel P as an orthogonal block reflector
-// Q' = I - V T V^T with Q'^T P = [R; 0], by nwg = ceil(M / 256) workgroups,
-// one thread per row, in three kernels (the kernel boundaries are the
-// panel-wide synchronisations, so no workgroup ever waits for another and
-// nothing requires co-residency -- several lanes' kernels share the chip):
-//   k_cqr_gram  per workgroup: the rows, their largest power-of-two exponent,
-//               the Gram partial of the prescaled rows
-//   k_cqr_q1    every workgroup: the partials summed in fixed order (each
-//               rescaled to the panel's exponent), R1 = chol(G1) (redundantly,
-//               wave 0), Q1 = P 2^-e R1^-1 for its rows (to the workspace),
-//               the Gram partial of Q1
-//   k_cqr_v     every workgroup: G2 = Q1^T Q1, R2 = chol(G2) (first order
-//               when G2 = I + E with |E| < 1e-8), V = Q = Q1 R2^-1 for its
-//               rows >= 32 (basis-kernel form: V = Q - [S; 0]); workgroup 0:
-//               the modified LU of the top block, Q_t - S = L U (s_j = -sign
-//               of the pivot, Ballard et al. 2015), V's top rows Q_t - S,
-//               T = -S (U^-1 L^-1)^T and the band block R = S R2 R1 2^e.
-// (Q' is orthogonal and Q' [S; 0] = Q for any sign matrix S with W_t = Q_t - S
-// invertible -- the basis-kernel representation of Sun and Bischof; the
-// modified LU's sign choice keeps W_t well conditioned, as in the Householder
-// reconstruction.)  All arithmetic in fp64.  A first-pass Cholesky pivot
-// that is not positive or below 1e-7 x the largest (panel condition number
-// beyond ~1e7, where CholeskyQR2 loses orthogonality) switches the panel to
-// shifted CholeskyQR3 (k_cqr_q1's shift, cqr_shifted_pass); a breakdown
-// after that sets the error word (3).
-// ==========================================================================
-constexpr int kCT = 256;
-constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
-constexpr int kCW = 64;   // most workgroups per panel (M <= kCW kCT rows)
-constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace ([32][kQS]: a lane per row, coalesced)
-
-struct CqrArgs {
-    const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
-    int M;
-    void *vdst; long vsi, vst;        // V(i, t)
-    void *vdst2; long vsi2, vst2;     // optional second copy of V (null: none)
-    void *tout;                       // T (32 x 32)
-    void *apan; long asi, ast;        // the panel in A: (i, t)
-    double *ws;                       // scratch (cqr_ws_doubles)
-    int *err;
-};
-
-// scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
-// per-workgroup exponents, R1, the shifted-pass flag, and Q1 [32][kCW kCT]
-__host__ __device__ constexpr size_t cqr_ws_doubles() {
-    return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
-}
-// Q_t (qt) and the zero flag are read by the next read pass's finishing
-// workgroup (cqr_finish)
-__host__ __device__ constexpr size_t cqr_ws_qt() { return (size_t)3 * 1024 * kCW + kCW + 1024; }
-__host__ __device__ constexpr size_t cqr_ws_zero() { return cqr_ws_qt() + 1024 + 2; }
-struct CqrWs {
-    double *gp1, *gp2, *ew, *r1, *qt, *shifted, *zero, *q1;
-    __device__ explicit CqrWs(double *ws)
-        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
-          qt(ws + cqr_ws_qt()), shifted(ws + cqr_ws_qt() + 1024), zero(ws + cqr_ws_zero()),
-          q1(ws + cqr_ws_zero() + 2) {}
-};
-
-struct CqrLds {
-    // the 32 x 32 matrices first: their LDS addresses fit the 16-bit offset field
-    double g[32][kSP];       // reduced Gram
-    double r1[32][kSP];      // R1 (upper, row-major)
-    double r2[32][kSP];      // R2
-    double u[32][kSP];       // U of the top block's LU (upper)
-    double mm[32][kSP];      // L^-1
-    double tq[32][kSP];      // Q's top block; then L (strict lower)
-    double r1w[32][kSP];     // R1 in trsm_row's form; then U^-1
-    double r2w[32][kSP];     // R2^-1 (first order) or R2 in trsm_row's form
-    double sgn[32];
-    double scl[kCW];         // per-partial scale factors of the Gram sum
-    int e_w;
-    int flags;
-    double q[4][64][33];     // per-wave staging of 64 rows (Gram, coalesced stores); per-wave Gram partials
-};
-
-__device__ __forceinline__ double rdl(double v, int l) {   // lane l's value, wave-uniform
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
-                            __builtin_amdgcn_readlane(__double2loint(v), l));
-}
-
-// Gram partial of this wave's rows (one per lane) accumulated into gacc
-// (the three distinct 16 x 16 blocks of the symmetric 32 x 32)
-__device__ __forceinline__ void gram_wave(CqrLds &L, int w, int lane, const double (&x)[32], double (&gacc)[3][4]) {
-    typedef Mf<double>::v4 v4;
-#pragma unroll
-    for (int t = 0; t < 32; ++t) L.q[w][lane][t] = x[t];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int qq = lane >> 4, l15 = lane & 15;
-    v4 a00 = {gacc[0][0], gacc[0][1], gacc[0][2], gacc[0][3]};
-    v4 a01 = {gacc[1][0], gacc[1][1], gacc[1][2], gacc[1][3]};
-    v4 a11 = {gacc[2][0], gacc[2][1], gacc[2][2], gacc[2][3]};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int k = 4 * s + qq;
-        const double v0 = L.q[w][k][l15], v1 = L.q[w][k][16 + l15];
-        a00 = Mf<double>::mma(v0, v0, a00);
-        a01 = Mf<double>::mma(v0, v1, a01);
-        a11 = Mf<double>::mma(v1, v1, a11);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) { gacc[0][g] = a00[g]; gacc[1][g] = a01[g]; gacc[2][g] = a11[g]; }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Cholesky G = R^T R (R upper) by one wave, lane c holding column c in
-// registers, row j of R broadcast by readlanes; R and 1/diag into LDS.
-// False on a non-positive or tiny pivot.
-__device__ __forceinline__ bool chol_wave(const double (&G)[32][kSP], double (&R)[32][kSP], double (&Rw)[32][kSP], int lane) {
-    // lane c: column c in registers; row j of R goes through LDS (R itself)
-    // and comes back as 16-byte broadcast reads: no readlane per element
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    const int c = lane & 31;
-    double col[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) col[i] = G[i][c];
-    bool ok = true;
-    double dmax = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        const double piv = rdl(col[j], j);
-        const bool good = piv > 0 && piv < 1e300;
-        // 1/sqrt by the hardware estimate and two Newton steps (the division and
-        // IEEE square root sit on the 32-step chain)
-        const double pv = good ? piv : 1.0;
-        double invd = __builtin_amdgcn_rsq(pv);
-        invd = invd * fma(-0.5 * pv * invd, invd, 1.5);
-        invd = invd * fma(-0.5 * pv * invd, invd, 1.5);
-        const double d = pv * invd;
-        dmax = fmax(dmax, d);
-        if (!good || d < 1e-7 * dmax) ok = false;
-        const double r = col[j] * invd;   // R[j][c] (meaningful for c >= j)
-        if (lane < 32) {
-            R[j][c] = c >= j ? r : 0.0;
-            Rw[j][c] = c > j ? r : (c == j ? invd : 0.0);
-        }
-        if (j == 31) break;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        d2 rr[16];
-#pragma unroll
-        for (int p = (j + 1) / 2; p < 16; ++p) rr[p] = *(const d2 *)&R[j][2 * p];
-#pragma unroll
-        for (int i = j + 1; i < 32; ++i) col[i] = fma(-((i & 1) ? rr[i >> 1].y : rr[i >> 1].x), r, col[i]);
-    }
-    return ok;
-}
-
-// Modified LU of Q_t - S = L U (Ballard et al. 2015: s_j = -sign of the
-// pivot, so every pivot has |.| >= 1) by one wave, lane r holding row r
-// (lanes 32-63 mirror).  The pivot row is lane jj's registers, broadcast by
-// readlanes (measured: 27 k clocks for the 32 steps; the same loop with the
-// pivot row published in LDS by its owner and read back as 16-byte
-// broadcasts took 34 k).  On return lane r's rv holds row r of L (strict
-// lower, unit diagonal implied) and U (upper); sgn[j] = s_j (LDS).
-__device__ __forceinline__ void lu_wave(double (&rv)[32], double *sgn, int lane) {
-    const int r = lane & 31;
-#pragma unroll
-    for (int jj = 0; jj < 32; ++jj) {
-        double piv = rdl(rv[jj], jj);
-        const double sg = piv >= 0 ? -1.0 : 1.0;
-        piv -= sg;                                    // |piv| >= 1
-        double inv = __builtin_amdgcn_rcp(piv);
-        inv = fma(inv, fma(-piv, inv, 1.0), inv);
-        inv = fma(inv, fma(-piv, inv, 1.0), inv);
-        if (lane == 0) sgn[jj] = sg;
-        const bool below = r > jj;
-        const double l = rv[jj] * inv;
-        const double lb = below ? l : 0.0;   // rows <= jj: an exact no-op update, no selects
-#pragma unroll
-        for (int cc = jj + 1; cc < 32; ++cc) {
-            const double u = rdl(rv[cc], jj);
-            rv[cc] = fma(-lb, u, rv[cc]);
-            if (((cc - jj) & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bounds live scalar registers
-        }
-        rv[jj] = below ? l : (r == jj ? piv : rv[jj]);
-    }
-}
-
-// One 16 x 16 tile (ti, tj) of C = A B for 32 x 32 matrices in LDS, K range
-// [k0, 32) (k0 a multiple of 4: triangular operands skip their zero blocks).
-__device__ __forceinline__ Mf<double>::v4 tile_mm(const double (&A)[32][kSP], const double (&B)[32][kSP], int ti, int tj,
-                                                 int lane, int k0, int k1) {
-    const int q = lane >> 4, l15 = lane & 15;
-    Mf<double>::v4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int k = k0; k < k1; k += 4) acc = Mf<double>::mma(A[16 * ti + l15][k + q], B[k + q][16 * tj + l15], acc);
-    return acc;
-}
-__device__ __forceinline__ void tile_store(double (&C)[32][kSP], const Mf<double>::v4 &t, int ti, int tj, int lane) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) C[16 * ti + Mf<double>::crow(lane >> 4, g)][16 * tj + (lane & 15)] = t[g];
-}
-
-// x <- x R^-1, right-looking.  Rw: R (upper) with the reciprocal of its
-// diagonal in place of the diagonal, in LDS.  Row k + 1 of Rw is read (as
-// 16-byte pairs, a wave-uniform address: one LDS broadcast per pair) while
-// step k computes, so the reads' latency is hidden behind the FMAs.
-typedef double d2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void trsm_row(double (&x)[32], const double (&Rw)[32][kSP]) {
-    d2v cur[16], nxt[16];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) cur[p] = *(const d2v *)&Rw[0][2 * p];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        if (k + 1 < 32) {
-#pragma unroll
-            for (int p = (k + 1) / 2; p < 16; ++p) nxt[p] = *(const d2v *)&Rw[k + 1][2 * p];
-        }
-        x[k] *= (k & 1) ? cur[k >> 1].y : cur[k >> 1].x;
-        const double xk = x[k];
-#pragma unroll
-        for (int i = k + 1; i < 32; ++i) x[i] = fma(-xk, (i & 1) ? cur[i >> 1].y : cur[i >> 1].x, x[i]);
-        if (k + 1 < 32) {
-#pragma unroll
-            for (int p = (k + 1) / 2; p < 16; ++p) cur[p] = nxt[p];
-        }
-#ifndef BRD_TRSM_FREE   // A/B knob: 1 = no scheduling groups (the compiler's own order)
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // the next row's LDS reads first
-        __builtin_amdgcn_sched_group_barrier(0x2, 64, 0);     // then this step's VALU
-#endif
-    }
-}
-
-// x <- x Ri for an upper-triangular Ri in LDS (all products independent:
-// x[t] = sum_{k <= t} x[k] Ri[k][t], k ascending).
-__device__ __forceinline__ void umul_row(double (&x)[32], const double (&Ri)[32][kSP]) {
-    double acc[32];
-#pragma unroll
-    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        d2v rr[16];
-#pragma unroll
-        for (int p = k / 2; p < 16; ++p) rr[p] = *(const d2v *)&Ri[k][2 * p];
-#pragma unroll
-        for (int t = k; t < 32; ++t) acc[t] = fma(x[k], (t & 1) ? rr[t >> 1].y : rr[t >> 1].x, acc[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < 32; ++t) x[t] = acc[t];
-}
-
-// The cluster's Gram partials (workgroup-major [nwg][1024]) summed by every
-// workgroup on its own, in fixed order (deterministic), scaled by the
-// per-partial powers of two scl[k]: one cluster barrier per Gram instead of a
-// slice-sum, a second barrier and a read-back.
-__device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg) {
-    const int tid = threadIdx.x;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 0; k0 < nwg; k0 += 8) {
-        double v[8][4];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int kc = min(k0 + k, nwg - 1);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[k][u] = gp[(size_t)kc * 1024 + tid + kCT * u];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const double sk = k0 + k < nwg ? scl[k0 + k] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] = fma(sk, v[k][u], acc[u]);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int el = tid + kCT * u;
-        L.g[el >> 5][el & 31] = acc[u];
-    }
-}
-
-// this thread's row of P (zeros past M), as doubles
-template <typename T>
-__device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x)[32]) {
-    const T *src = (const T *)a.src;
-    const T *srow = src + (size_t)(i < a.M ? i : 0) * a.si;
-    if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
-        typedef typename G2<T>::v2 v2;
-#pragma unroll
-        for (int t = 0; t < 32; t += 2) {
-            const v2 v = *(const v2 *)(srow + t);
-            x[t] = (double)v.x;
-            x[t + 1] = (double)v.y;
-        }
-    } else {
-        const long st = a.st;
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = (double)srow[t * st];
-    }
-    if (i >= a.M) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = 0.0;
-    }
-}
-
-// Gram partial of the workgroup's rows (one per thread) -> dst (1024 doubles):
-// the four waves' partials summed in fixed order
-__device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32], double *dst) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    double gacc[3][4] = {};
-    gram_wave(L, w, lane, x, gacc);
-    __syncthreads();
-    double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);   // [4][32][33] over the staging
-    const int qq = lane >> 4, l15 = lane & 15;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int rr = Mf<double>::crow(qq, g);
-        gw[w][rr][l15] = gacc[0][g];
-        gw[w][rr][16 + l15] = gacc[1][g];
-        gw[w][16 + l15][rr] = gacc[1][g];
-        gw[w][16 + rr][16 + l15] = gacc[2][g];
-    }
-    __syncthreads();
-    for (int el = tid; el < 1024; el += kCT) {
-        const int i = el >> 5, t = el & 31;
-        dst[el] = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
-    }
-}
-
-// the panel's exponent e (INT_MIN: the panel is zero) and the partials' scale
-// factors 2^(2 (e_k - e)) into L.scl
-__device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg, bool ones) {
-    const int tid = threadIdx.x;
-    __shared__ int ewl[kCW];
-    if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[tid] : INT_MIN;
-    __syncthreads();
-    int e = INT_MIN;
-    for (int k = 0; k < nwg; ++k) e = max(e, ewl[k]);
-    if (tid < kCW) L.scl[tid] = ones ? 1.0 : ((tid < nwg && ewl[tid] != INT_MIN) ? ldexp(1.0, 2 * (ewl[tid] - e)) : 0.0);
-    __syncthreads();
-    return e;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
-    __shared__ CqrLds L;
-    const int tid = threadIdx.x, lane = tid & 63, wg = blockIdx.x;
-    CqrWs W(a.ws);
-    double x[32];
-    cqr_load_row<T>(a, wg * kCT + tid, x);
-    double m = 0;
-#pragma unroll
-    for (int t = 0; t < 32; ++t) m = fmax(m, fabs(x[t]));
-    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) L.e_w = INT_MIN;
-    __syncthreads();
-    if (lane == 0) {
-        int e = INT_MIN;
-        if (m > 0) frexp(m, &e);
-        atomicMax(&L.e_w, e);
-    }
-    __syncthreads();
-    const int e_w = L.e_w;
-    if (e_w != INT_MIN) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e_w);
-    }
-    cqr_gram_partial(L, x, W.gp1 + (size_t)wg * 1024);
-    if (tid == 0) W.ew[wg] = (double)e_w;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
-    __shared__ CqrLds L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
-    CqrWs W(a.ws);
-    if (tid == 0) L.flags = 0;
-    const int i = wg * kCT + tid;
-    double x[32];
-    cqr_load_row<T>(a, i, x);   // in flight under the Gram sum and the Cholesky
-    const int e = cqr_exponent(L, W.ew, nwg, false);
-    if (e == INT_MIN) {   // zero panel: k_cqr_v writes V = [I; 0], T = 0, R = 0
-        if (wg == 0 && tid == 0) W.shifted[0] = 0.0;
-        return;
-    }
-    gram_sum_all(L, W.gp1, L.scl, nwg);
-    __syncthreads();
-#if BRD_DIAG_Q1 == 2
-    if (wg >= 0) return;
-#endif
-    if (w == 0) {
-        bool good = chol_wave(L.g, L.r1, L.r1w, lane);
-        if (!good) {
-            // an ill-conditioned panel (cond > ~1e7, e.g. numerically rank
-            // deficient): the shifted Cholesky of sCQR3 (Fukaya et al. 2020),
-            // G + s I with s = 11 (32 M + 32 33) u tr(G); then Q1 has
-            // cond ~ 1e3 and k_cqr_v's cqr_shifted_pass re-orthogonalises it once more
-            double tr = 0;
-#pragma unroll
-            for (int k = 0; k < 32; ++k) tr += L.g[k][k];
-            const double sh = 11.0 * (32.0 * a.M + 32.0 * 33.0) * 0x1p-53 * tr;
-            if (lane < 32) L.g[lane][lane] += sh;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            good = chol_wave(L.g, L.r1, L.r1w, lane);
-            if (lane == 0) L.flags = good ? 2 : 1;
-        }
-    }
-    __syncthreads();
-#if BRD_DIAG_Q1 == 1
-    if (wg >= 0) return;
-#endif
-    if (L.flags == 1 && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wg == 0) {
-        for (int el = tid; el < 1024; el += kCT) W.r1[el] = L.r1[el >> 5][el & 31];
-        if (tid == 0) W.shifted[0] = L.flags == 2 ? 1.0 : 0.0;
-    }
-    // Q1 = (P 2^-e) R1^-1
-#pragma unroll
-    for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e);
-    trsm_row(x, L.r1w);
-    if (i >= a.M) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = 0.0;
-    }
-#pragma unroll
-    for (int t = 0; t < 32; ++t) W.q1[t * kQS + i] = x[t];
-    cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
-}
-
-// After a shifted first pass only (W.shifted): sCQR3's middle pass, run by
-// every workgroup of k_cqr_v on its own (the same reads in the same order,
-// so the same result everywhere; no kernel of its own, which the common
-// unshifted panel would pay for as a launch): R = chol(Q1^T Q1), the Gram of
-// Q1 R^-1 over ALL rows into L.g (the four waves' sums in fixed order),
-// R R1 into L.r1 and this thread's row of Q1 R^-1 into x.  Every workgroup
-// walks all rows (the rare ill-conditioned panel pays ~0.1-0.2 ms).
-__device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, int M, int nwg, double (&x)[32]) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    gram_sum_all(L, W.gp2, L.scl, nwg);
-    __syncthreads();
-    if (w == 0) {
-        const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
-        if (lane == 0 && !good) L.flags = 1;
-    }
-    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
-    __syncthreads();
-    double gacc[3][4] = {};
-    for (int chunk = 0; chunk < nwg; ++chunk) {
-        const int i = chunk * kCT + tid;
-        double y[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) y[t] = W.q1[t * kQS + i];
-        trsm_row(y, L.r2w);
-        if (i >= M) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) y[t] = 0.0;
-        }
-        if (chunk == (int)blockIdx.x) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) x[t] = y[t];
-        }
-        gram_wave(L, w, lane, y, gacc);
-    }
-    // R R1 (waves 0-3: one tile each, into registers first: L.r1 is an operand)
-    Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
-    const int ti = w >> 1, tj = w & 1;
-    if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
-        L.r1[i2][c] = i2 <= c ? rt[g] : 0.0;
-    }
-    double(*gw)[32][33] = reinterpret_cast<double(*)[32][33]>(&L.q[0][0][0]);
-    const int qq = lane >> 4, l15 = lane & 15;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int rr = Mf<double>::crow(qq, g);
-        gw[w][rr][l15] = gacc[0][g];
-        gw[w][rr][16 + l15] = gacc[1][g];
-        gw[w][16 + l15][rr] = gacc[1][g];
-        gw[w][16 + rr][16 + l15] = gacc[2][g];
-    }
-    __syncthreads();
-    for (int el = tid; el < 1024; el += kCT) {
-        const int i2 = el >> 5, t = el & 31;
-        L.g[i2][t] = (gw[0][i2][t] + gw[1][i2][t]) + (gw[2][i2][t] + gw[3][i2][t]);
-    }
-}
-
-// --------------------------------------------------------------------------
-// cqr_finish: the rest of a panel's reconstruction, run by the first
-// workgroup of the read pass that follows the panel (k_rpass), beside the
-// pass itself -- the read pass uses V' = Q (the modified LU's signs enter
-// only V's top block, and Y_j = A^T V_j T_j is corrected by prep).  Wave 0:
-// the modified LU of Q_t - S = L U (s_j = -sign of the pivot); then wave 1
-// U^-1, wave 2 L^-1, wave 3 the band block R = S R' in place; then every
-// wave one tile of T = -S (U^-1 L^-1)^T.  A zero panel gets S = -I, T = 0.
-// All 512 threads of the workgroup pass the barriers; waves 4-7 idle.
-// --------------------------------------------------------------------------
-struct FinArgs {
-    const double *qt;     // Q_t (32 x 32, row-major)
-    const double *zero;   // 1: the panel was zero
-    double *sgn;          // out: s_j
-    void *tout;           // out: T
-    void *apan; long asi, ast;   // the band block R' (in place -> S R')
-};
-struct FinLds {
-    double u[32][kSP];       // U (upper)
-    double tq[32][kSP];      // Q_t, then L (strict lower)
-    double ui[32][kSP];      // U^-1
-    double li[32][kSP];      // L^-1
-    double sgn[32];
-};
-
-// (LDS matrices passed separately: k_cqr_v's inline use maps them onto its
-// own; tq_loaded: Q_t is already in tq)
-template <typename T>
-__device__ __forceinline__ void cqr_finish(double (&Lu)[32][kSP], double (&Ltq)[32][kSP], double (&Lui)[32][kSP],
-                                           double (&Lli)[32][kSP], double *Lsgn, const FinArgs &f, int tid,
-                                           bool tq_loaded) {
-    const int lane = tid & 63, w = tid >> 6;
-    const bool zero = f.zero[0] != 0.0;
-    if (!tq_loaded)
-        for (int el = tid; el < 1024; el += blockDim.x) Ltq[el >> 5][el & 31] = f.qt[el];
-    __syncthreads();
-    if (w == 0) {
-        const int r = lane & 31;
-        double rv[32];
-#pragma unroll
-        for (int cc = 0; cc < 32; ++cc) rv[cc] = Ltq[r][cc];
-        if (!zero) {
-            lu_wave(rv, Lsgn, lane);
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < 32; ++jj) rv[jj] = r == jj ? 1.0 : 0.0;
-            if (lane < 32) Lsgn[lane] = -1.0;
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int cc = 0; cc < 32; ++cc) Lu[r][cc] = cc >= r ? rv[cc] : 0.0;
-#pragma unroll
-            for (int cc = 0; cc < 32; ++cc) Ltq[r][cc] = cc < r ? rv[cc] : 0.0;
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-        if (lane < 32) f.sgn[lane] = Lsgn[lane];
-    } else if (w == 1) {
-        // U^-1 (lane c = column c, right-looking back substitution)
-        const int c = lane & 31;
-        double acc[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 31; k >= 0; --k) {
-            const double d = Lu[k][k];
-            double inv = __builtin_amdgcn_rcp(d);
-            inv = fma(inv, fma(-d, inv, 1.0), inv);
-            inv = fma(inv, fma(-d, inv, 1.0), inv);
-            const double xk = acc[k] * inv;
-            acc[k] = xk;
-#pragma unroll
-            for (int i2 = 0; i2 < k; ++i2) acc[i2] = fma(-Lu[i2][k], xk, acc[i2]);
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) Lui[k][c] = acc[k];
-        }
-    } else if (w == 2) {
-        // L^-1 (unit lower; lane c = column c, forward substitution)
-        const int c = lane & 31;
-        double acc[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) acc[k] = k == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            const double xk = acc[k];
-#pragma unroll
-            for (int i2 = k + 1; i2 < 32; ++i2) acc[i2] = fma(-Ltq[i2][k], xk, acc[i2]);
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) Lli[k][c] = acc[k];
-        }
-    } else if (w == 3) {
-        // R = S R' (upper block, rows scaled by s_i)
-        T *ap = (T *)f.apan;
-        for (int el = lane; el < 1024; el += 64) {
-            const int i2 = el >> 5, c = el & 31;
-            if (i2 <= c) {
-                T *pp = ap + (size_t)i2 * f.asi + (size_t)c * f.ast;
-                *pp = (T)(Lsgn[i2] * (double)*pp);
-            }
-        }
-    }
-    __syncthreads();
-    if (w < 4) {
-        // T = -S (U^-1 L^-1)^T: wave w forms tile (w >> 1, w & 1) of U^-1 L^-1
-        const int ti = w >> 1, tj = w & 1;
-        const Mf<double>::v4 pt = tile_mm(Lui, Lli, ti, tj, lane, 16 * (ti > tj ? ti : tj), 32);
-        T *tout = (T *)f.tout;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), j2 = 16 * tj + (lane & 15);
-            tout[j2 * 32 + i2] = (T)(zero ? 0.0 : -Lsgn[j2] * pt[g]);
-        }
-    }
-}
-
-template <typename T>
-__device__ void cqr_finish_entry(const FinArgs &f, int tid, void *lds) {
-    static_assert(sizeof(FinLds) <= kRpLds * sizeof(double), "cqr_finish's LDS exceeds the read pass's block");
-    FinLds &FL = *reinterpret_cast<FinLds *>(lds);
-    cqr_finish<T>(FL.u, FL.tq, FL.ui, FL.li, FL.sgn, f, tid, false);
-}
-
-// INLINE (the last LQ panel of a block, whose U's top block the block update
-// reads straight away): workgroup 0 also runs cqr_finish itself and patches
-// V's top block to Q_t - S in place.
-template <typename T, bool INLINE>
-__global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_cqr_v(CqrArgs a, FinArgs fin) {
-    __shared__ CqrLds L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
-    CqrWs W(a.ws);
-    if (tid == 0) L.flags = 0;
-    const int e = cqr_exponent(L, W.ew, nwg, true);
-    const bool zero = e == INT_MIN;   // V = [I; 0], T = 0, R = 0
-    const int i = wg * kCT + tid;
-    T *ap = (T *)a.apan;
-    T *vd = (T *)a.vdst;
-    T *vd2 = (T *)a.vdst2;
-    double x[32];
-    const bool sh = !zero && W.shifted[0] != 0.0;
-    if (!zero && !sh) {   // this thread's row of Q1, in flight under the Gram sum
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = W.q1[t * kQS + i];
-    }
-    if (!zero) {
-        if (sh) cqr_shifted_pass(L, W, a.M, nwg, x);
-        else    gram_sum_all(L, W.gp2, L.scl, nwg);
-        __syncthreads();
-        // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
-        // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
-        // half its diagonal) and its inverse I - U1 + O(E^2): both to working
-        // accuracy, without the 32-step factorization.  Every wave decides
-        // (the same reads, the same result).
-        bool fast;
-        {
-            const int c = lane & 31, i0 = (lane >> 5) * 16;
-            double em = 0;
-#pragma unroll
-            for (int ii = 0; ii < 16; ++ii) em = fmax(em, fabs(L.g[i0 + ii][c] - (i0 + ii == c ? 1.0 : 0.0)));
-            for (int o = 32; o >= 1; o >>= 1) em = fmax(em, __shfl_xor(em, o, 64));
-            fast = em < 1e-8;   // uniform over the workgroup
-        }
-        if (fast) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int el = tid + kCT * u, r = el >> 5, c = el & 31;
-                const double u1 = r < c ? L.g[r][c] : (r == c ? 0.5 * (L.g[c][c] - 1.0) : 0.0);
-                L.r2[r][c] = (r == c ? 1.0 : 0.0) + u1;
-                L.r2w[r][c] = (r == c ? 1.0 : 0.0) - u1;
-            }
-        } else if (w == 0) {
-            const bool good = chol_wave(L.g, L.r2, L.r2w, lane);
-            if (lane == 0 && !good) L.flags = 1;
-        }
-        __syncthreads();
-        // Q = Q1 R2^-1, this thread's row
-        if (fast) umul_row(x, L.r2w);
-        else      trsm_row(x, L.r2w);
-        if (i >= a.M) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) x[t] = 0.0;
-        }
-    } else {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) x[t] = 0.0;
-    }
-    if (wg == 0 && tid < 32) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) L.tq[tid][t] = x[t];   // Q_t for the LU
-    }
-
-    // ---- V's rows into vdst (and vdst2), zeros into the panel's rows >= 32.
-    // Destinations with unit column stride are written coalesced: the wave's
-    // 64 rows are staged in its LDS tile and each store instruction covers 4
-    // rows x 32 contiguous elements (a lane per row would touch 64 rows per
-    // instruction).  Rows in [rlo, rhi) of this wave only.
-    const int wrow0 = wg * kCT + 64 * w;   // first row of this wave
-    auto store_v = [&](const double (&v)[32], int rlo, int rhi) {
-        typedef typename G2<T>::v2 v2;
-        const bool mine = i >= rlo && i < rhi && i < a.M;
-        if (a.vst == 1 || (vd2 && a.vst2 == 1)) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) L.q[w][lane][t] = v[t];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        auto rowmajor = [&](T *base, long rs) {
-#pragma unroll 4
-            for (int it = 0; it < 16; ++it) {
-                const int r = 4 * it + (lane >> 4), row = wrow0 + r, cp = 2 * (lane & 15);
-                if (row >= rlo && row < rhi && row < a.M)
-                    *(v2 *)(base + (size_t)row * rs + cp) = v2{(T)L.q[w][r][cp], (T)L.q[w][r][cp + 1]};
-            }
-        };
-        if (a.vst == 1) rowmajor(vd, a.vsi);
-        else if (mine) {
-            T *vr = vd + (size_t)i * a.vsi;
-#pragma unroll
-            for (int t = 0; t < 32; ++t) vr[t * a.vst] = (T)v[t];
-        }
-        if (vd2) {
-            if (a.vst2 == 1) rowmajor(vd2, a.vsi2);
-            else if (mine) {
-                T *vr2 = vd2 + (size_t)i * a.vsi2;
-#pragma unroll
-                for (int t = 0; t < 32; ++t) vr2[t * a.vst2] = (T)v[t];
-            }
-        }
-    };
-    store_v(x, 0, INT_MAX);   // V' = Q (the top rows get - S after the LU: k_vsum)
-    {   // zeros below the panel's R block
-        typedef typename G2<T>::v2 v2;
-        if (a.ast == 1) {
-#pragma unroll 4
-            for (int it = 0; it < 16; ++it) {
-                const int row = wrow0 + 4 * it + (lane >> 4), cp = 2 * (lane & 15);
-                if (row >= 32 && row < a.M) *(v2 *)(ap + (size_t)row * a.asi + cp) = v2{(T)0, (T)0};
-            }
-        } else if (i >= 32 && i < a.M) {
-            T *arow = ap + (size_t)i * a.asi;
-#pragma unroll
-            for (int t = 0; t < 32; ++t) arow[t * a.ast] = (T)0;
-        }
-    }
-    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wg != 0) return;
-
-    // ---- workgroup 0: Q_t and the zero flag for the LU (k_rpass's finishing
-    // workgroup), and R' = R2 R1 2^e into the panel (its rows get S there) ----
-    if (tid < 32) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) W.qt[tid * 32 + t] = x[t];
-    }
-    if (tid == 0) W.zero[0] = zero ? 1.0 : 0.0;
-    if (w == 3) {
-        if (!sh)   // (after a shifted pass L.r1 already holds R R1)
-            for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4) {
-            const int ti = t4 >> 1, tj = t4 & 1;
-            Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
-            if (tj >= ti && !zero) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
-                ap[(size_t)i2 * a.asi + (size_t)c * a.ast] = (T)(i2 <= c ? ldexp(rt[g], e) : 0.0);
-            }
-        }
-    }
-    if constexpr (INLINE) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // R' and Q_t stores landed (read back below)
-        __syncthreads();
-        cqr_finish<T>(L.u, L.tq, L.r1w, L.mm, L.sgn, fin, tid, true);
-        __syncthreads();
-        if (tid < 32) {   // V's top block: Q_t - S on the diagonal, both copies
-            T *p1 = vd + (size_t)tid * a.vsi + (size_t)tid * a.vst;
-            *p1 = (T)((double)*p1 - L.sgn[tid]);
-            if (vd2) {
-                T *p2 = vd2 + (size_t)tid * a.vsi2 + (size_t)tid * a.vst2;
-                *p2 = (T)((double)*p2 - L.sgn[tid]);
-            }
-        }
-    }
-}
-
-
-// ==========================================================================
-// k_blkupd: C[r][c] -= sum_{k < 256} Lw[r][k] RwT[k][c] for r >= r0, c >= c0:
-// the block's delayed rank-256 update on the matrix cores.  Workgroup tile
-// 128 x 128 (4 waves of 64 x 64: 16 accumulator tiles of 16 x 16), K in
-// chunks of 16 through double-buffered LDS (Lw: pair-swizzled [kp][r][2];
-// RwT: [k][c] with a 144-element pitch), the C tile in the accumulators.
-// ==========================================================================
-constexpr int kGT = 256;
-constexpr int kGM = 128;
-constexpr int kGKC = 16;
-constexpr int kGBP = kGM + 16;
-
-struct GemmArgs {
-    void *C; long ldc;
-    int rows, cols;                 // extent of the updated region
-    const void *Lw; const void *RwT; long ldr;
-    int K;                          // 256
-    int tiles_c;                    // column tiles
-    int ntiles;                     // tiles (the grid may be padded)
-};
-
-template <typename T>
-struct GemmLds {
-    T a[2][kGKC * kGM];     // Lw tile, pair-swizzled
-    T b[2][kGKC * kGBP];    // RwT tile
-};
-
-template <typename T>
-__global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
-    typedef typename G2<T>::v2 v2;
-    typedef typename Mf<T>::v4 v4;
-    __shared__ GemmLds<T> L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int q = lane >> 4, l15 = lane & 15;
-#ifndef BRD_BLK_SWZ
-#define BRD_BLK_SWZ 0   // A/B knob: > 0 = tile order in groups of that many tile rows per XCD
-#endif
-    int tr, tc;
-    if constexpr (BRD_BLK_SWZ > 0) {
-        // XCD-aware order: workgroup b runs on XCD b % 8 (dispatch round-robin);
-        // each XCD takes its own contiguous eighth of the tiles and walks them
-        // in groups of BRD_BLK_SWZ tile rows, sweeping the columns, so a group's
-        // Lw rows and the current RwT column tile stay in that XCD's L2
-        // (the grid is padded to a multiple of 8; the padding workgroups exit)
-        const int nt = a.ntiles, per = (int)gridDim.x / 8;
-        const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-        const int tt = xcd * per + loc;
-        if (tt >= nt) return;
-        const int tiles_r = nt / a.tiles_c;
-        const int G = BRD_BLK_SWZ, grp = tt / (G * a.tiles_c), rem = tt % (G * a.tiles_c);
-        const int gr = min(G, tiles_r - grp * G);
-        tr = grp * G + rem % gr;
-        tc = rem / gr;
-    } else {
-        tr = blockIdx.x / a.tiles_c;
-        tc = blockIdx.x % a.tiles_c;
-    }
-    const int r0 = tr * kGM, c0 = tc * kGM;
-    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
-    T *C = (T *)a.C;
-    const T *Lw = (const T *)a.Lw;
-    const T *RwT = (const T *)a.RwT;
-
-    // C tile into the accumulators
-    v4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int r = r0 + wr + 16 * i + Mf<T>::crow(q, g), cc = c0 + wc + 16 * j + l15;
-                acc[i][j][g] = (r < a.rows && cc < a.cols) ? C[(size_t)r * a.ldc + cc] : (T)0;
-            }
-
-    // per chunk: Lw 128 x 16 (1024 granules), RwT 16 x 128 (1024 granules): 4 + 4 per thread
-    auto load = [&](int k0, v2 (&ga)[4], v2 (&gb)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = tid + kGT * i;
-            const int r = e >> 3, kp = e & 7;
-            const int rg = r0 + r;
-            ga[i] = rg < a.rows ? *(const v2 *)(Lw + (size_t)rg * 256 + k0 + 2 * kp) : v2{(T)0, (T)0};
-            const int k = e >> 6, cp = e & 63;
-            const int cg = c0 + 2 * cp;
-            v2 v = {(T)0, (T)0};
-            if (cg < a.cols) {
-                const T *p = RwT + (size_t)(k0 + k) * a.ldr + cg;
-                if (cg + 1 < a.cols) v = *(const v2 *)p; else v.x = p[0];
-            }
-            gb[i] = v;
-        }
-    };
-    auto stage = [&](int buf, const v2 (&ga)[4], const v2 (&gb)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = tid + kGT * i;
-            const int r = e >> 3, kp = e & 7;
-            // negated: the MFMA adds A B to the C tile
-            *(v2 *)&L.a[buf][2 * (kp * kGM + (r ^ kp))] = v2{-ga[i].x, -ga[i].y};
-            const int k = e >> 6, cp = e & 63;
-            *(v2 *)&L.b[buf][k * kGBP + 2 * cp] = gb[i];
-        }
-    };
-    const int nc = a.K / kGKC;
-    v2 ga[4], gb[4];
-    load(0, ga, gb);
-    for (int c = 0; c < nc; ++c) {
-        stage(c & 1, ga, gb);
-        lds_barrier();
-        if (c + 1 < nc) load((c + 1) * kGKC, ga, gb);
-#pragma unroll
-        for (int s = 0; s < kGKC / 4; ++s) {
-            const int k = 4 * s + q, kp = k >> 1, hf = k & 1;
-            T av[4], bv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = wr + 16 * i + l15;
-                av[i] = L.a[c & 1][2 * (kp * kGM + (r ^ kp)) + hf];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[j] = L.b[c & 1][k * kGBP + wc + 16 * j + l15];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int r = r0 + wr + 16 * i + Mf<T>::crow(q, g), cc = c0 + wc + 16 * j + l15;
-                if (r < a.rows && cc < a.cols) C[(size_t)r * a.ldc + cc] = acc[i][j][g];
-            }
-}
-
-}  // namespace blk
 
 // --------------------------------------------------------------------------
 // Host side
@@ -1709,19 +81,6 @@ int blk_columns(int m, int n, int b) {
     return k0;
 }
 
-// Every launch of the blocked path goes through here: with brd_profile on,
-// the launch itself stamps its start and end (hipExtLaunchKernel), tagged with
-// the kernel's algorithmic flops and HBM bytes (bench.py's roofline objects).
-template <typename F, typename... Args>
-static void blk_launch(const char *kind, double flops, double bytes, F kernel, dim3 grid, dim3 block, hipStream_t s,
-                       Args... args) {
-    hipEvent_t ea, eb;
-    if (api_prof_launch_events(kind, flops, bytes, &ea, &eb))
-        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ea, eb, 0, args...);
-    else
-        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
-}
-
 // the prep kernels' grid: split K halves (kPI items per workgroup) while
 // that grid fits the CUs the stream may use (one workgroup per CU: LDS),
 // else 2 kPI items per workgroup, one K range per wave
@@ -1756,14 +115,11 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.has_fin = fin ? 1 : 0;
     const FinArgs fa = fin ? *fin : FinArgs{};
     *ksplit_out = ks;
-    dim3 grid(a.has_fin + a.nvirt + a.mtiles * ks), block(kRT);
+    dim3 grid(a.has_fin + a.nvirt + a.mtiles * ks);
     // algorithmic: the K x M source read once, 2 x 32 flops per element
     const double fl = 2.0 * 32 * K * M, by = (double)K * M * sizeof(T);
-    if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true, FinArgs>, grid, block, s, a, fa);
-    else    blk_launch("s1_rpass", fl, by, k_rpass<T, false, FinArgs>, grid, block, s, a, fa);
-    if (a.nvirt > 0)
-        blk_launch("s1_prep", 0.0, 0.0, k_vsum<T>, dim3(32 * kMT / 256), dim3(256), s, (const T *)a.vpart, (T *)a.vout,
-                   a.nvirt, pbase, pstride, psgn);
+    launch_k_rpass<T>(yp, grid, a, fa, s, fl, by);
+    if (a.nvirt > 0) launch_k_vsum<T>((const T *)a.vpart, (T *)a.vout, a.nvirt, pbase, pstride, psgn, s);
     return hipGetLastError();
 }
 
@@ -1780,10 +136,9 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     if (nwg > Ly.cwg) return hipErrorInvalidValue;
     a.ws = (double *)(ws + Ly.cws);
     a.err = err;
-    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a);
-    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a);
-    if (inl) blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, true>, dim3(nwg), dim3(kCT), s, a, fin);
-    else     blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, false>, dim3(nwg), dim3(kCT), s, a, fin);
+    launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);
+    launch_k_cqr<T>(kCqrQ1, nwg, a, fin, s);
+    launch_k_cqr<T>(inl ? kCqrVInline : kCqrV, nwg, a, fin, s);
     return hipGetLastError();
 }
 
@@ -1835,7 +190,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
-                blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, prep_grid(p, target), dim3(kPT), s, p);
+                launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -1856,7 +211,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
-                blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, prep_grid(p, target), dim3(kPT), s, p);
+                launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -1884,7 +239,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
-            blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, prep_grid(p, target), dim3(kPT), s, p);
+            launch_k_prep<T>(false, prep_grid(p, target), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -1897,11 +252,10 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             g.tiles_c = (g.cols + kGM - 1) / kGM;
             const int tiles_r = (g.rows + kGM - 1) / kGM;
             g.ntiles = tiles_r * g.tiles_c;
-            const int grid = BRD_BLK_SWZ > 0 ? (g.ntiles + 7) / 8 * 8 : g.ntiles;
+            const int grid = g.ntiles;
             // algorithmic: C read and written once, Lw / RwT read once; 2 x 256 flops per element
             const double el = (double)g.rows * g.cols;
-            blk_launch("s1_blkupd", 2.0 * 256 * el, (2.0 * el + 256.0 * (g.rows + g.cols)) * sizeof(T), k_blkupd<T>,
-                       dim3(grid), dim3(kGT), s, g);
+            launch_k_blkupd<T>(dim3(grid), g, s, 2.0 * 256 * el, (2.0 * el + 256.0 * (g.rows + g.cols)) * sizeof(T));
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -66,7 +66,7 @@ def test_extreme_scale_is_scale_invariant(S, T, scale, tol):
     the band, and s^-1 times the reduction of s A close to the reduction of A
     (tol 1e-3 / 1e-2); at 2^480 the squares stay normal and the reduction is
     scale-invariant to rounding (1e-12).  n = 300: the blocked stage 1 on the
-    first 128 columns, the per-panel path after; stage 2 in the
+    first 256 columns (blk_columns(300, 300, 32) = 256), the per-panel path after; stage 2 in the
     sigma-preserving geometry, compared through the singular values."""
     n, b = 300, 32
     A = np.random.default_rng(3).uniform(1, 5, (n, n)).astype(T)
@@ -86,13 +86,20 @@ def test_extreme_scale_is_scale_invariant(S, T, scale, tol):
     assert np.max(np.abs(sv_s - sv)) <= 10 * tol * sv[-1], np.max(np.abs(sv_s - sv)) / sv[-1]
 
 
-@pytest.mark.parametrize("kind", ["perm", "zero_cols", "rank1"])
+@pytest.mark.parametrize("kind", ["perm", "zero_cols", "rank1", "zero_col_in_panel", "dup_cols", "rank1_exact",
+                                  "rank20_exact", "dup_rows"])
 def test_structured_panels(S, kind):
     """Panels whose orthonormal factor has a permutation-like top block (the
     case the modified LU's sign choice exists for: with a fixed sign the
     reconstruction's W_t = Q_t - S would be singular), exactly zero panels,
-    and a rank-deficient input.  Stage 1 must keep exact zeros outside the
-    band and the input's singular values (fp64, 1e-12 sigma_max)."""
+    and rank-deficient inputs: a rank-1 matrix plus 1e-8 noise, and EXACTLY
+    rank-deficient panels -- one zero column inside a non-zero
+    panel, duplicated columns (and rows: the LQ side), an exact rank-1 outer
+    product, an exact rank-20 product -- where the first CholeskyQR pass and
+    then sCQR3's middle pass meet a zero pivot and the panel's basis is
+    completed (cqr_shifted_pass).  Stage 1 (the blocked path: n = 512 reduces
+    columns 0..383 blocked) must keep exact zeros outside the band and the
+    input's singular values (fp64, 1e-12 sigma_max), and report no error."""
     n, b = 512, 32
     rng = np.random.default_rng(17)
     if kind == "perm":
@@ -104,8 +111,25 @@ def test_structured_panels(S, kind):
         A = rng.uniform(1, 5, (n, n))
         A[:, :b] = 0.0
         A[:, 3 * b:5 * b] = 0.0
-    else:
+    elif kind == "rank1":
         A = np.outer(rng.standard_normal(n), rng.standard_normal(n)) + 1e-8 * rng.standard_normal((n, n))
+    elif kind == "zero_col_in_panel":
+        A = rng.uniform(1, 5, (n, n))
+        A[:, 5] = 0.0
+        A[:, 200] = 0.0
+    elif kind == "dup_cols":
+        A = rng.uniform(1, 5, (n, n))
+        A[:, 7] = A[:, 3]
+        A[:, 40] = A[:, 33]
+        A[:, 300] = A[:, 290]
+    elif kind == "dup_rows":
+        A = rng.uniform(1, 5, (n, n))
+        A[9] = A[2]
+        A[100] = A[60]
+    elif kind == "rank1_exact":
+        A = np.outer(rng.standard_normal(n), rng.standard_normal(n))
+    else:
+        A = rng.standard_normal((n, 20)) @ rng.standard_normal((20, n))
     ref = np.linalg.svd(A, compute_uv=False)
     band = S.brd_p1(A, b)
     assert np.all(np.isfinite(band))

@@ -544,6 +544,12 @@ bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEve
 }
 void api_lock() { g_ctx.mu.lock(); }
 void api_unlock() { g_ctx.mu.unlock(); }
+int *api_s1_err() {
+    int *e = nullptr;
+    return ensure_s1_err(&e) == BRD_OK ? e : nullptr;
+}
+int api_take_s1_error(int *code) { return take_s1_error(slot(), code); }
+const char *api_err_text(int code) { return err_word_text(code); }
 
 // --------------------------------------------------------------------------
 // host/device staging shared by both stages

@@ -89,6 +89,12 @@ struct PrepArgs {
     int reduce, factor;       // QR side switches
     const double *sgn;        // s_t of the panel whose pass preceded (V' = Q was used: corrections)
     int split;                // 1: kPI items, K1 in two halves; 0: 2 kPI items, one K range
+    long cc;                  // column base in A and RwT: LQ the column of item 0 (c + 32 on one
+                              // GPU, the rank's first local trailing column when the columns are
+                              // sharded); QR the panel's first column (c; its local column)
+    int qprow;                // LQ: 1 = the corrected panel stored [item][32] (the distributed
+                              // path's all-gather slot), 0 = transposed [32][mq]
+    int zfill;                // LQ, qprow: items [items, zfill) stored as zero rows (slot padding)
 };
 
 constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
@@ -98,7 +104,8 @@ constexpr int kQP = 40;    // QR pitch (rows k, k + 2 in opposite bank halves)
 // ---- k_cqr_* (brd_blk_cqr.hip) ----------------------------------------------
 constexpr int kCT = 256;
 constexpr int kSP = 34;   // pitch of the 32 x 32 LDS matrices (even: 16-byte pairs)
-constexpr int kCW = 64;   // most workgroups per panel (M <= kCW kCT rows)
+constexpr int kCW = 128;  // most workgroups per panel (M <= kCW kCT rows; the distributed LQ panel
+                          // is padded per rank: P x roundup(local columns, 256) rows)
 constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace ([32][kQS]: a lane per row, coalesced)
 
 struct CqrArgs {
@@ -110,6 +117,9 @@ struct CqrArgs {
     void *apan; long asi, ast;        // the panel in A: (i, t)
     double *ws;                       // scratch (cqr_ws_doubles)
     int *err;
+    int azero;                        // 1: zeros into the panel's rows >= 32 (apan); 0: the caller zeroes
+    double *qcopy;                    // optional copy of Q_t (1024 doubles, row-major) and the zero-panel
+                                      // flag (element 1024): the distributed path's broadcast (null: none)
 };
 
 // scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
@@ -291,8 +301,9 @@ __device__ __forceinline__ void cqr_finish(double (&Lu)[32][kSP], double (&Ltq)[
 #pragma unroll
             for (int k = 0; k < 32; ++k) Lli[k][c] = acc[k];
         }
-    } else if (w == 3) {
-        // R = S R' (upper block, rows scaled by s_i)
+    } else if (w == 3 && f.apan) {
+        // R = S R' (upper block, rows scaled by s_i; the distributed path: on
+        // the rank holding the band block only)
         T *ap = (T *)f.apan;
         for (int el = lane; el < 1024; el += 64) {
             const int i2 = el >> 5, c = el & 31;
@@ -365,6 +376,14 @@ template <typename T>
 void launch_k_cqr(CqrKernel which, int nwg, const CqrArgs &a, const FinArgs &f, hipStream_t s);
 template <typename T>
 void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, double by);
+// the distributed path's data movement (brd_blk_comm.hip)
+template <typename T>
+void launch_dist_unpack_v(const T *src, T *dst, int M, hipStream_t s);
+template <typename T>
+void launch_dist_scatter_u(const T *Vg, long base, int nc, T *RwT, long ldr, int rrow, long lcs, T *Ub, T *A, long lda,
+                           int c, int z0, hipStream_t s);
+template <typename T>
+void launch_dist_psum(const T *part, int ks, long mp, int rows, T *buf, hipStream_t s);
 
 }  // namespace blk
 }  // namespace brd

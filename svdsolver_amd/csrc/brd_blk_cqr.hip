@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         }
     };
     store_v(x, 0, INT_MAX);   // V' = Q (the top rows get - S after the LU: k_vsum)
-    {   // zeros below the panel's R block
+    if (a.azero) {   // zeros below the panel's R block
         typedef typename G2<T>::v2 v2;
         if (a.ast == 1) {
 #pragma unroll 4
@@ -628,7 +628,14 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         for (int t = 0; t < 32; ++t) W.qt[tid * 32 + t] = x[t];
     }
     if (tid == 0) W.zero[0] = zero ? 1.0 : 0.0;
-    if (w == 3) {
+    if (a.qcopy) {
+        if (tid < 32) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) a.qcopy[tid * 32 + t] = x[t];
+        }
+        if (tid == 0) a.qcopy[1024] = zero ? 1.0 : 0.0;
+    }
+    if (w == 3 && ap) {
         if (!sh)   // (after a shifted pass L.r1 already holds R R1)
             for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

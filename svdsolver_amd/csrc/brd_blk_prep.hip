@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     const int i0 = blockIdx.x * (a.split ? kPI : 2 * kPI) + 16 * wi;
     const int il = i0 + l15;                       // this lane's item (B operand / C column)
     const bool iv = il < a.items;
-    const long col = (long)c + 32 + il;
+    const long col = a.cc + il;
     const T *A = (const T *)a.A;
     v4 ay[2], aq[2];
 #pragma unroll
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     // (rows [128, 128 + 32j)); all B operands are loaded before the first MFMA
     // (unconditional loads at clamped addresses, zeroed when out of range)
     constexpr int kMS = 8 * (NBMAX - 1);   // most steps per K1 range (j <= NBMAX - 1)
-    const long colc = iv ? col : (long)c + 32;
+    const long colc = iv ? col : a.cc;
     T bk[2][kMS];
 #pragma unroll
     for (int pp = 0; pp < 2; ++pp)
@@ -205,7 +205,11 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int t = 16 * h + Mf<T>::crow(q, g);
-            if (iv) QpT[(size_t)t * a.mq + il] = aq[h][g];
+            if (a.qprow) {
+                if (il < a.zfill) QpT[(size_t)il * 32 + t] = iv ? aq[h][g] : (T)0;
+            } else if (iv) {
+                QpT[(size_t)t * a.mq + il] = aq[h][g];
+            }
         }
 }
 
@@ -239,7 +243,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ic = i0 + Mf<T>::crow(q, g);
-            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + c + 16 * h + l15] : (T)0;
+            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + a.cc + 16 * h + l15] : (T)0;
         }
     // ranges of Lw columns: [0, 32j) (compact 0; K half 0) and [128, 128 + 32jp)
     // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
@@ -271,7 +275,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
         const int kk = tid, k = kk < 32 * j ? kk : 128 + kk - 32 * j;
         T v[32];
 #pragma unroll
-        for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + c + t];
+        for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + a.cc + t];
 #pragma unroll
         for (int t = 0; t < 32; ++t) Rs[kk * kQP + t] = -v[t];
     }

@@ -146,14 +146,6 @@ namespace {
 // ==========================================================================
 // communicators
 // ==========================================================================
-struct Comm {
-    int rank = 0, nranks = 1;
-    virtual ~Comm() {}
-    virtual int bcast(void *buf, size_t bytes, int root, hipStream_t s) = 0;
-    virtual int allgather(const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
-    virtual int allreduce_sum(void *buf, size_t count, int dtype, hipStream_t s) = 0;
-};
-
 int rccl_fail(ncclResult_t r, const char *what) {
     std::string m = std::string(what) + ": " + ncclGetErrorString(r);
     return api_fail(BRD_ERCCL, m.c_str());
@@ -229,15 +221,8 @@ CommReg g_comms;
 // layout helpers
 // ==========================================================================
 int npanels(int n, int b) { return (n + b - 1) / b; }
-// panels p < g with p mod P == r
-int panels_before(int g, int P, int r) { return g > r ? (g - r + P - 1) / P : 0; }
-int local_cols(int n, int b, int P, int r) {
-    const int np = npanels(n, b);
-    const int cnt = panels_before(np, P, r);
-    if (cnt == 0) return 0;
-    const int last = (cnt - 1) * P + r;   // last global panel of rank r
-    return (cnt - 1) * b + std::min(b, n - last * b);
-}
+int panels_before(int g, int P, int r) { return dist_panels_before(g, P, r); }
+int local_cols(int n, int b, int P, int r) { return dist_local_cols(n, b, P, r); }
 
 // ==========================================================================
 // workspace
@@ -287,6 +272,18 @@ int dtype_of() { return sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32; }
 // ==========================================================================
 // the distributed panel loop
 // ==========================================================================
+// The blocked form (brd_stage1_blk.hip, blk_ge2band_dist) over the columns
+// it covers: b = 32, fp64 (its panel QR computes in fp64 whatever the input,
+// as on one GPU), unless BRD_S1_BLOCKED=0; BRD_DIST_BLOCKED=0 keeps the
+// per-panel loop throughout (A/B).
+template <typename T>
+int dist_blocked_columns(int m, int n, int lda, int b, const T *A) {
+    const char *e1 = getenv("BRD_S1_BLOCKED"), *e2 = getenv("BRD_DIST_BLOCKED");
+    if ((e1 && e1[0] == '0') || (e2 && e2[0] == '0')) return 0;
+    if (sizeof(T) != 8 || b != 32 || lda % 2 != 0 || ((uintptr_t)A % 16) != 0) return 0;
+    return blk_columns(m, n, b);
+}
+
 template <typename T>
 int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
     Comm &C = *g_comms.find(s);
@@ -294,6 +291,13 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
     const int P = C.nranks, me = C.rank;
     const int n_loc = local_cols(n, b, P, me);
     if (lda < std::max(n_loc, 1)) return api_fail(BRD_EINVAL, "lda_loc smaller than the local column count");
+    const int kend = dist_blocked_columns<T>(m, n, lda, b, A);
+    if (kend > 0) {
+        int *err = api_s1_err();
+        if (!err) return api_fail(BRD_ENOMEM, "stage-1 error word allocation failed");
+        D_TRY(g_dws.ensure(blk_dist_ws_bytes(m, n, P, me, sizeof(T)), s));
+        D_TRY(blk_ge2band_dist<T>(A, m, n, lda, C, g_dws.mem, s, api_apply_target(), err));
+    }
     if (P * b > kRmax) return api_fail(BRD_EUNSUPPORTED, "nranks * b must be <= 512 (one-level tree root)");
     const size_t sz = sizeof(T);
     // workspace: QR / local-LQ tree, root tree, panel, local R, gathered R, stack, W
@@ -314,7 +318,7 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
 
     TreeWs ws, wsr;
     const int np = npanels(n, b);
-    for (int k = 0; k < np; ++k) {
+    for (int k = kend / b; k < np; ++k) {
         const int kb = k * b, bk = std::min(b, n - kb), mp = m - kb, n2 = n - kb - bk;
         const int owner = k % P;
         const int lc_k = (k / P) * b;                       // owner's local column of panel k
@@ -453,7 +457,15 @@ int ge2band_dist_entry(T *A, int m, int n, int lda, int b, unsigned flags) {
     if (b < 1 || b > kBmax) return api_fail(BRD_EINVAL, "band width outside [1, 32]");
     if (!(flags & BRD_DEVICE_PTR)) return api_fail(BRD_EINVAL, "distributed stage 1 takes device pointers (BRD_DEVICE_PTR)");
     int rc = ge2band_dist<T>(A, m, n, lda, b, s);
-    if (rc == BRD_OK && !(flags & BRD_ASYNC)) D_HIP(hipStreamSynchronize(s));
+    if (rc == BRD_OK && !(flags & BRD_ASYNC)) {
+        D_HIP(hipStreamSynchronize(s));
+        int code = 0;
+        D_TRY(api_take_s1_error(&code));
+        if (code) {
+            std::string msg = std::string("distributed stage 1: ") + api_err_text(code);
+            return api_fail(BRD_EHIP, msg.c_str());
+        }
+    }
     return rc;
 }
 

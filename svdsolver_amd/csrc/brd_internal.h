@@ -70,6 +70,36 @@ int blk_columns(int m, int n, int b);
 template <typename T>
 hipError_t blk_ge2band(T *A, int m, int n, long lda, void *ws, hipStream_t s, int target, int *err);
 
+// ---- multi-GPU (brd_dist.hip) -------------------------------------------------
+// Collectives on device buffers, enqueued on (or drained from) stream s:
+// RCCL over xGMI, or host callbacks (tests).  Return BRD_OK or a brd_status
+// with brd_last_error set.
+struct Comm {
+    int rank = 0, nranks = 1;
+    virtual ~Comm() {}
+    virtual int bcast(void *buf, size_t bytes, int root, hipStream_t s) = 0;
+    virtual int allgather(const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
+    virtual int allreduce_sum(void *buf, size_t count, int dtype, hipStream_t s) = 0;
+};
+// 1-D block-cyclic layout over column panels of width b: global panel p on
+// rank p mod P.  Panels p' < g on rank r, and rank r's column count.
+inline int dist_panels_before(int g, int P, int r) { return g > r ? (g - r + P - 1) / P : 0; }
+inline int dist_local_cols(int n, int b, int P, int r) {
+    const int np = (n + b - 1) / b;
+    const int cnt = dist_panels_before(np, P, r);
+    if (cnt == 0) return 0;
+    const int last = (cnt - 1) * P + r;
+    return (cnt - 1) * b + (n - last * b < b ? n - last * b : b);
+}
+
+// Blocked stage 1 sharded over the ranks of C (b = 32, fp64): columns [0,
+// blk_columns(m, n, 32)) of the global matrix; A is this rank's m x n_loc
+// shard.  ws: blk_dist_ws_bytes.  The caller finishes the remaining panels
+// with the per-panel distributed loop.
+size_t blk_dist_ws_bytes(int m, int n, int P, int rank, size_t elem);
+template <typename T>
+int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *ws, hipStream_t s, int target, int *err);
+
 // Stage-2 launchers (brd_stage2.hip).
 template <typename T>
 hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool sigma_geom, int *prog, int *err,
@@ -98,6 +128,11 @@ bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEve
 bool api_take_launch_events(hipEvent_t *start, hipEvent_t *stop);
 void api_lock();
 void api_unlock();
+// The current stream's stage-1 device error word (allocated on first use),
+// and a synchronous read-and-clear of it (0: no error).
+int *api_s1_err();
+int api_take_s1_error(int *code);
+const char *api_err_text(int code);
 // Stage-1 panel helpers shared with the single-GPU loop.
 long tree_level_rows(const Tree &t, int level);
 

@@ -25,6 +25,7 @@
 // tests/s1_model.py; DESIGN.md "Stage 1, blocked" has the roofline of each
 // kernel.  This file is the host driver; the kernels live in brd_blk_*.hip
 // (brd_blk.h).
+#include "brd.h"
 #include "brd_blk.h"
 
 #include <algorithm>
@@ -85,16 +86,17 @@ int blk_columns(int m, int n, int b) {
 // that grid fits the CUs the stream may use (one workgroup per CU: LDS),
 // else 2 kPI items per workgroup, one K range per wave
 static dim3 prep_grid(PrepArgs &p, int cus) {
-    const int n1 = (p.items + kPI - 1) / kPI;
+    const int items = std::max(p.items, p.qprow ? p.zfill : 0);
+    const int n1 = (items + kPI - 1) / kPI;
     p.split = n1 <= cus ? 1 : 0;
-    return dim3(p.split ? n1 : (p.items + 2 * kPI - 1) / (2 * kPI));
+    return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 
 template <typename T>
 static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
                                long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
                                int target, int *ksplit_out, const FinArgs *fin, T *pbase, long pstride,
-                               const double *psgn) {
+                               const double *psgn, void *vout = nullptr) {
     RpArgs a;
     a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
     a.K = K; a.M = M;
@@ -109,7 +111,7 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.ksplit = ks;
     a.nvirt = vsrc ? ks : 0;
     a.part = ws + Ly.part; a.mp = Ly.mp;
-    a.vpart = ws + Ly.vpart; a.vout = ws + Ly.vout;
+    a.vpart = ws + Ly.vpart; a.vout = vout ? vout : ws + Ly.vout;
     a.counter = counter;
     a.err = err;
     a.has_fin = fin ? 1 : 0;
@@ -126,7 +128,7 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
 template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
-                             hipStream_t s, bool inl, const FinArgs &fin) {
+                             hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr) {
     CqrArgs a;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
@@ -136,6 +138,8 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     if (nwg > Ly.cwg) return hipErrorInvalidValue;
     a.ws = (double *)(ws + Ly.cws);
     a.err = err;
+    a.azero = azero;
+    a.qcopy = qcopy;
     launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);
     launch_k_cqr<T>(kCqrQ1, nwg, a, fin, s);
     launch_k_cqr<T>(inl ? kCqrVInline : kCqrV, nwg, a, fin, s);
@@ -190,6 +194,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
+                p.cc = c; p.qprow = 0; p.zfill = 0;
                 launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -211,6 +216,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
+                p.cc = c + 32; p.qprow = 0; p.zfill = 0;
                 launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -239,6 +245,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
+            p.cc = k1; p.qprow = 0; p.zfill = 0;
             launch_k_prep<T>(false, prep_grid(p, target), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -265,5 +272,191 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
 
 template hipError_t blk_ge2band<double>(double *, int, int, long, void *, hipStream_t, int, int *);
 template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStream_t, int, int *);
+
+// ==========================================================================
+// The blocked path sharded over P GPUs (brd_dist.hip's
+// layout: global column panel p on rank p mod P).  Lw = [V | X] (m x 256) is
+// replicated, RwT = [Y | U] and Ub hold this rank's columns; the block update
+// k_blkupd is local to each rank's columns.  Per panel j (global panel p,
+// column c), three collectives:
+//   QR   the owner of panel p forms the corrected column panel (k_prep_qr,
+//        after every rank has added X_{j-1} to its Lw from the all-reduced
+//        X partials) and runs its CholeskyQR; V' = Q (m - c rows), Q_t and
+//        the zero flag are BROADCAST; every rank finishes the reconstruction
+//        (modified LU, T_j, signs) beside its own Y pass, which is local:
+//        Y_j = A^T V_j T_j needs only this rank's columns (svd_cuda_2.cu:1184,
+//        qr_apply_cuda's column loop, sharded by columns).
+//   LQ   every rank corrects its columns of the row panel (k_prep_lq) into
+//        its slot of an ALL-GATHER (slots padded to a multiple of 256 rows);
+//        every rank runs the same CholeskyQR on the gathered panel, rotated
+//        so that panel p+1's columns (the band block, on rank (p+1) mod P)
+//        come first, and finishes inline -- identical U_j, S_j everywhere;
+//        each rank keeps its rows of U_j (k_dist_scatter_u).
+//   X    X_j = A U_j S_j sums over columns: each rank's split-K partials
+//        (and its part of G = Rw^T U_j) are summed locally (k_dist_psum) and
+//        ALL-REDUCED (m - c - 32 + 256 rows of 32).
+// Message sizes per panel: m x 32 (broadcast), n x 32 in total (all-gather),
+// (m + 256) x 32 (all-reduce) -- against the per-panel path's m x b
+// broadcast + P b^2 gather + b x m all-reduce, but 2.5 passes over the
+// trailing matrix per 32 columns instead of 4, the update on the matrix cores.
+// ==========================================================================
+namespace {
+struct DistBlk {
+    size_t bc, gat, vg, ar, total;
+    long cnt;   // rows per all-gather slot
+};
+DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
+    const BlkLayout Ly = blk_layout(m, std::max(dist_local_cols(n, 32, P, rank), 1), elem);
+    int nmax = 0;
+    for (int r = 0; r < P; ++r) nmax = std::max(nmax, dist_local_cols(n, 32, P, r));
+    DistBlk D;
+    D.cnt = std::max(256L, ((long)nmax + 255) / 256 * 256);
+    size_t off = Ly.total;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    D.bc = take((size_t)m * 32 * elem + 1032 * sizeof(double));   // V' rows, then Q_t + zero flag
+    D.gat = take((size_t)2 * P * D.cnt * 32 * elem);              // gathered slots + rotation tail
+    D.vg = take((size_t)P * D.cnt * 32 * elem);                   // the gathered panel's basis
+    D.ar = take(((size_t)m * 32 + 256 * 32) * elem);              // G (256 x 32), then X rows
+    D.total = off;
+    return D;
+}
+}  // namespace
+
+size_t blk_dist_ws_bytes(int m, int n, int P, int rank, size_t elem) { return dist_blk_layout(m, n, P, rank, elem).total; }
+
+#define BD_HIP(expr)                                                                          \
+    do {                                                                                      \
+        const hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                               \
+            char m_[256];                                                                     \
+            snprintf(m_, sizeof m_, "blocked distributed stage 1: %s (%s:%d)", hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                                     \
+            return api_fail(BRD_EHIP, m_);                                                    \
+        }                                                                                     \
+    } while (0)
+#define BD_TRY(expr)             \
+    do {                         \
+        const int rc_ = (expr);  \
+        if (rc_) return rc_;     \
+    } while (0)
+
+template <typename T>
+int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream_t s, int target, int *err) {
+    const int P = C.nranks, me = C.rank;
+    const int n_loc = dist_local_cols(n, 32, P, me);
+    const int kend = blk_columns(m, n, 32);
+    char *ws = (char *)wsv;
+    const BlkLayout Ly = blk_layout(m, std::max(n_loc, 1), sizeof(T));
+    const DistBlk D = dist_blk_layout(m, n, P, me, sizeof(T));
+    const long cnt = D.cnt;
+    T *Lw = (T *)(ws + Ly.lw), *RwT = (T *)(ws + Ly.rwt), *Ub = (T *)(ws + Ly.ub);
+    T *tf = (T *)(ws + Ly.tf);
+    int *ctr = (int *)(ws + Ly.ctr);
+    const long ldr = Ly.ldr;
+    T *bc = (T *)(ws + D.bc), *gat = (T *)(ws + D.gat), *Vg = (T *)(ws + D.vg), *ar = (T *)(ws + D.ar);
+    const int dt = sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32;
+    BD_HIP(hipMemsetAsync(ctr, 0, 64 * sizeof(int), s));
+    double *sgq = (double *)(ws + Ly.sg), *sgl = sgq + NBMAX * 32, *sg0 = sgq + 2 * NBMAX * 32;
+    BD_HIP(hipMemsetAsync(sg0, 0, 32 * sizeof(double), s));
+    const double *cws = (const double *)(ws + Ly.cws);
+    auto prep = [&](int c, int j, int items, int reduce, int factor, const void *part, long mp, int ks, const void *G,
+                    const T *Tm, const double *sgn, long cc) {
+        PrepArgs p;
+        p.A = A; p.lda = lda; p.Lw = Lw; p.RwT = RwT; p.ldr = ldr;
+        p.part = part; p.mp = mp; p.ksplit = ks; p.G = G; p.Tm = Tm;
+        p.Qp = ws + Ly.qp; p.mq = Ly.mp;
+        p.c = c; p.j = j; p.items = items; p.reduce = reduce; p.factor = factor;
+        p.sgn = sgn; p.cc = cc; p.qprow = 0; p.zfill = 0;
+        return p;
+    };
+    for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
+        for (int j = 0; j < NBMAX; ++j) {
+            const int p = k0 / 32 + j, c = 32 * p, mr = m - c, mx = m - c - 32;
+            const int o = p % P, o2 = (p + 1) % P;          // owners of panel p and of panel p + 1
+            const bool own = me == o, own2 = me == o2;
+            const long lco = (long)(p / P) * 32;            // panel p's column on its owner
+            const long lcs = (long)dist_panels_before(p + 1, P, me) * 32;   // first local trailing column
+            const int nc = n_loc - (int)lcs;                 // local trailing columns
+            T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
+            double *qt = (double *)((char *)bc + (size_t)mr * 32 * sizeof(T));   // Q_t, zero flag
+            // ---- X_{j-1} (every rank) + the column panel's QR (its owner) ----------
+            if (j > 0) {
+                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1),
+                                   sg0, lco);
+                launch_k_prep<T>(false, prep_grid(pa, target), pa, s);
+                BD_HIP(hipGetLastError());
+            }
+            const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
+            if (own) {
+                const T *src = j == 0 ? A + (size_t)c * lda + lco : (const T *)(ws + Ly.qp);
+                const long si = j == 0 ? lda : 1, st = j == 0 ? 1 : Ly.mp;
+                BD_HIP(launch_cqr<T>(src, si, st, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, bc, 32, 1, Tj,
+                                     A + (size_t)c * lda + lco, lda, 1, ws, Ly, err, s, false, fq, 1, qt));
+            }
+            if (P > 1) {
+                BD_TRY(C.bcast(bc, (size_t)mr * 32 * sizeof(T) + 1025 * sizeof(double), o, s));
+                if (!own) launch_dist_unpack_v<T>(bc, Lw + (size_t)c * 256 + 32 * j, mr, s);
+            }
+            // ---- Y pass (local columns; every rank finishes the QR panel) -----------
+            int ks_y = 1;
+            BD_HIP(launch_rpass<T>(true, A + (size_t)c * lda + lcs, lda, mr, nc, Lw + (size_t)c * 256 + 32 * j, 256,
+                                   Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
+                                   Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j));
+            // ---- the row panel: corrected locally, gathered, factored everywhere ----
+            T *slot = gat + (size_t)me * cnt * 32;
+            {
+                PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
+                pa.Qp = slot; pa.qprow = 1; pa.zfill = (int)cnt;
+                launch_k_prep<T>(true, prep_grid(pa, target), pa, s);
+                BD_HIP(hipGetLastError());
+            }
+            if (P > 1) BD_TRY(C.allgather(slot, gat, (size_t)cnt * 32 * sizeof(T), s));
+            if (o2 != 0)   // rotate: panel p+1's slot first (its first 32 rows are the band block's columns)
+                BD_HIP(hipMemcpyAsync(gat + (size_t)P * cnt * 32, gat, (size_t)o2 * cnt * 32 * sizeof(T),
+                                      hipMemcpyDeviceToDevice, s));
+            const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
+                             own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
+            BD_HIP(launch_cqr<T>(gat + (size_t)o2 * cnt * 32, 32, 1, (int)(P * cnt), Vg, 32, 1, nullptr, 0, 0, Sj,
+                                 own2 ? A + (size_t)c * lda + lcs : nullptr, 1, lda, ws, Ly, err, s, true, fl, 0));
+            launch_dist_scatter_u<T>(Vg, (long)((me - o2 + P) % P) * cnt, nc, RwT, ldr, 128 + 32 * j, lcs, Ub, A, lda,
+                                     c, own2 ? 32 : 0, s);
+            // ---- X pass (local columns), partials summed and all-reduced ------------
+            if (nc > 0) {
+                int ks_x = 1;
+                BD_HIP(launch_rpass<T>(false, A + (size_t)(c + 32) * lda + lcs, lda, nc, mx, Ub + lcs * 32, 32,
+                                       RwT + lcs, ldr, ws, Ly, ctr + 16, err, s, target, &ks_x, nullptr, nullptr, 0,
+                                       nullptr, ar));
+                launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
+            } else {
+                BD_HIP(hipMemsetAsync(ar, 0, ((size_t)mx * 32 + 256 * 32) * sizeof(T), s));
+            }
+            if (P > 1) BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32, dt, s));
+        }
+        // ---- block end: X_3 (every rank), the rank-256 update of my columns ---------
+        const int k1 = k0 + NBMAX * 32;
+        {
+            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
+            launch_k_prep<T>(false, prep_grid(pa, target), pa, s);
+            BD_HIP(hipGetLastError());
+        }
+        const long lck = (long)dist_panels_before(k1 / 32, P, me) * 32;
+        const int cols = n_loc - (int)lck;
+        if (cols > 0) {
+            GemmArgs g;
+            g.C = A + (size_t)k1 * lda + lck; g.ldc = lda;
+            g.rows = m - k1; g.cols = cols;
+            g.Lw = Lw + (size_t)k1 * 256; g.RwT = RwT + lck; g.ldr = ldr;
+            g.K = 256;
+            g.tiles_c = (g.cols + kGM - 1) / kGM;
+            g.ntiles = ((g.rows + kGM - 1) / kGM) * g.tiles_c;
+            const double el = (double)g.rows * g.cols;
+            launch_k_blkupd<T>(dim3(g.ntiles), g, s, 2.0 * 256 * el, (2.0 * el + 256.0 * (g.rows + g.cols)) * sizeof(T));
+            BD_HIP(hipGetLastError());
+        }
+    }
+    return BRD_OK;
+}
+template int blk_ge2band_dist<double>(double *, int, int, long, Comm &, void *, hipStream_t, int, int *);
+template int blk_ge2band_dist<float>(float *, int, int, long, Comm &, void *, hipStream_t, int, int *);
 
 }  // namespace brd

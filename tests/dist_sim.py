@@ -63,13 +63,14 @@ def panels_before(g, P, r):
     return (g - r + P - 1) // P if g > r else 0
 
 
-def ge2band_dist_sim(A_loc, n, b, rank, P, dist, group=None):
-    """Distributed dense -> band on this rank's shard (numpy, in place)."""
+def ge2band_dist_sim(A_loc, n, b, rank, P, dist, group=None, k_start=0):
+    """Distributed dense -> band on this rank's shard (numpy, in place), from
+    global panel k_start on."""
     import torch
     m = A_loc.shape[0]
     n_loc = A_loc.shape[1]
     np_ = (n + b - 1) // b
-    for k in range(np_):
+    for k in range(k_start, np_):
         kb = k * b
         bk = min(b, n - kb)
         mp, n2 = m - kb, n - kb - bk

@@ -94,6 +94,51 @@ def _sim_worker(rank, world, port, n, b, seed, out_path):
     tdist.destroy_process_group()
 
 
+def _blk_sim_worker(rank, world, port, n, b, seed, out_path):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
+    import torch.distributed as tdist
+    import dist_blk_sim
+    from svdsolver_amd import dist
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    A = np.random.default_rng(seed).uniform(1, 5, (n, n))
+    loc = dist.shard(A, b, world, rank).astype(np.float64)
+    dist_blk_sim.ge2band_blk_dist_sim(loc, n, b, rank, world, tdist)
+    wmax = max(dist.local_cols(n, b, world, r) for r in range(world))
+    mine = np.zeros((n, wmax))
+    mine[:, :loc.shape[1]] = loc
+    parts = [torch.zeros((n, wmax), dtype=torch.float64) for _ in range(world)]
+    tdist.all_gather(parts, torch.from_numpy(mine))
+    if rank == 0:
+        shards = [parts[r].numpy()[:, :dist.local_cols(n, b, world, r)] for r in range(world)]
+        np.save(out_path, dist.unshard(shards, n, b))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 512), (3, 600), (4, 704)])
+def test_blocked_distributed_algorithm_gloo(world, n, tmp_path):
+    """The blocked distributed stage 1's data flow (tests/dist_blk_sim.py:
+    owner-side column-panel QR + broadcast, local Y pass, gathered row panel
+    factored on every rank, all-reduced X pass, local block update; b = 32,
+    blocks of 4 panels, the per-panel tail after) on 2-4 gloo ranks: the band
+    matches the single-process blocked model (tests/s1_model.py) in |.| and
+    keeps the singular values (fp64, 1e-12)."""
+    import torch.multiprocessing as mp
+    import s1_model
+    b = 32
+    out = str(tmp_path / "band.npy")
+    mp.spawn(_blk_sim_worker, args=(world, _free_port(), n, b, 11, out), nprocs=world, join=True)
+    band = np.load(out)
+    A = np.random.default_rng(11).uniform(1, 5, (n, n))
+    ref = s1_model.ge2band_blocked(A, b)
+    assert _band_err(band, ref, b) <= 1e-12
+    assert np.all(np.abs(band[~_band_mask(n, b)]) < 1e-12 * np.abs(ref).max())
+    sa, sb = np.linalg.svd(A, compute_uv=False), np.linalg.svd(band, compute_uv=False)
+    assert np.max(np.abs(sa - sb)) <= 1e-12 * sa[0]
+
+
 @pytest.mark.parametrize("world,n,b", [(2, 96, 8), (3, 100, 8), (2, 130, 32)])
 def test_distributed_algorithm_gloo(world, n, b, tmp_path):
     import torch.multiprocessing as mp
@@ -148,8 +193,18 @@ def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path, root=0):
     (3, 600, 32, np.float64, "host"),     # ragged last panel (600 = 18 * 32 + 24)
     (2, 512, 16, np.float32, "host"),
     (1, 512, 32, np.float64, "rccl"),
+    # the blocked distributed path over >= 5 panels: 2 blocks of
+    # 4 panels at 1024, 8 at 1100 with a ragged tail, 4 ranks
+    (2, 1024, 32, np.float64, "host"),
+    (3, 1100, 32, np.float64, "host"),
+    (4, 1024, 32, np.float64, "host"),
+    (1, 1024, 32, np.float64, "rccl"),
 ])
 def test_distributed_stage1_gpu(world, n, b, dtype, mode, tmp_path):
+    """Against the single-GPU stage 1 (|band|, fp64 1e-12): with b = 32 in
+    fp64 the columns the blocked path covers (blk_columns) run the blocked
+    distributed form (brd_stage1_blk.hip blk_ge2band_dist), the rest the
+    per-panel distributed loop."""
     import torch.multiprocessing as mp
     import svdsolver_amd as S
     out = str(tmp_path / "band.npy")

@@ -416,6 +416,12 @@ def main():
     # MI355X pool, HIP's own default).
     if args.lanes > 1:
         want = min(32, 2 * args.lanes + 4)
+        # across GPUs every lane's stage-1 stream also carries an RCCL
+        # communicator, whose internal streams take hardware queues too
+        # (rocprofv3 trace at world size 1, 8 lanes: 53 streams on 20 queues,
+        # stage-2 streams sharing queues with other lanes' stage 1): all 32
+        if args.mode == "dist" and (args.force_dist or int(os.environ.get("WORLD_SIZE", "1")) > 1):
+            want = 32
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
@@ -628,6 +634,7 @@ def main():
     rp = S.profile_query("s1_rpass")
     cq = S.profile_query("s1_cqr")
     pp = S.profile_query("s1_prep")
+    cm = S.profile_query("s1_comm")   # the distributed blocked path's data movement around its collectives
     blocked = bu["launches"] > 0
 
     flops_per = 8.0 / 3.0 * n ** 3
@@ -700,6 +707,7 @@ def main():
                                    "s1_rpass": round(rp["ms"] / args.steps, 3),
                                    "s1_panel_cqr": round(cq["ms"] / args.steps, 3),
                                    "s1_prep": round(pp["ms"] / args.steps, 3),
+                                   "s1_comm": round(cm["ms"] / args.steps, 3),
                                    "s1_apply": round(ap["ms"] / args.steps, 3),
                                    "s1_factor": round(fa["ms"] / args.steps, 3),
                                    "s2_sweep": round(sw["ms"] / args.steps, 3)},

@@ -92,9 +92,8 @@ struct PrepArgs {
     long cc;                  // column base in A and RwT: LQ the column of item 0 (c + 32 on one
                               // GPU, the rank's first local trailing column when the columns are
                               // sharded); QR the panel's first column (c; its local column)
-    int qprow;                // LQ: 1 = the corrected panel stored [item][32] (the distributed
-                              // path's all-gather slot), 0 = transposed [32][mq]
-    int zfill;                // LQ, qprow: items [items, zfill) stored as zero rows (slot padding)
+    int zfill;                // LQ: items [items, zfill) of Qp stored as zeros (the distributed
+                              // path's all-gather slot padding)
 };
 
 constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)
@@ -120,6 +119,9 @@ struct CqrArgs {
     int azero;                        // 1: zeros into the panel's rows >= 32 (apan); 0: the caller zeroes
     double *qcopy;                    // optional copy of Q_t (1024 doubles, row-major) and the zero-panel
                                       // flag (element 1024): the distributed path's broadcast (null: none)
+    long blk, bstride;                // blk > 0: the source is stored in blocks of blk rows (a multiple of
+                                      // kCT), block q at src + q bstride, row i of it at (i mod blk) si
+                                      // (the distributed path's gathered [rank][32][slot] row panel)
 };
 
 // scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the

@@ -215,7 +215,9 @@ __device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const 
 template <typename T>
 __device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x)[32]) {
     const T *src = (const T *)a.src;
-    const T *srow = src + (size_t)(i < a.M ? i : 0) * a.si;
+    const int ic = i < a.M ? i : 0;
+    const T *srow = a.blk > 0 ? src + (size_t)(ic / a.blk) * a.bstride + (size_t)(ic % a.blk) * a.si
+                              : src + (size_t)ic * a.si;
     if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
         typedef typename G2<T>::v2 v2;
 #pragma unroll

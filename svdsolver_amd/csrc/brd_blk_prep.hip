@@ -205,11 +205,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int t = 16 * h + Mf<T>::crow(q, g);
-            if (a.qprow) {
-                if (il < a.zfill) QpT[(size_t)il * 32 + t] = iv ? aq[h][g] : (T)0;
-            } else if (iv) {
-                QpT[(size_t)t * a.mq + il] = aq[h][g];
-            }
+            if (iv || il < a.zfill) QpT[(size_t)t * a.mq + il] = iv ? aq[h][g] : (T)0;
         }
 }
 

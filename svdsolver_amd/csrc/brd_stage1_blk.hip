@@ -86,7 +86,7 @@ int blk_columns(int m, int n, int b) {
 // that grid fits the CUs the stream may use (one workgroup per CU: LDS),
 // else 2 kPI items per workgroup, one K range per wave
 static dim3 prep_grid(PrepArgs &p, int cus) {
-    const int items = std::max(p.items, p.qprow ? p.zfill : 0);
+    const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
     p.split = n1 <= cus ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
@@ -128,7 +128,8 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
 template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
-                             hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr) {
+                             hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr,
+                             long blk = 0, long bstride = 0) {
     CqrArgs a;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
@@ -140,6 +141,7 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.err = err;
     a.azero = azero;
     a.qcopy = qcopy;
+    a.blk = blk; a.bstride = bstride;
     launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);
     launch_k_cqr<T>(kCqrQ1, nwg, a, fin, s);
     launch_k_cqr<T>(inl ? kCqrVInline : kCqrV, nwg, a, fin, s);
@@ -194,7 +196,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
-                p.cc = c; p.qprow = 0; p.zfill = 0;
+                p.cc = c; p.zfill = 0;
                 launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -216,7 +218,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.Qp = ws + Ly.qp; p.mq = Ly.mp;
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
-                p.cc = c + 32; p.qprow = 0; p.zfill = 0;
+                p.cc = c + 32; p.zfill = 0;
                 launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -245,7 +247,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.Qp = ws + Ly.qp; p.mq = Ly.mp;
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
-            p.cc = k1; p.qprow = 0; p.zfill = 0;
+            p.cc = k1; p.zfill = 0;
             launch_k_prep<T>(false, prep_grid(p, target), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -287,7 +289,9 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 //        Y_j = A^T V_j T_j needs only this rank's columns (svd_cuda_2.cu:1184,
 //        qr_apply_cuda's column loop, sharded by columns).
 //   LQ   every rank corrects its columns of the row panel (k_prep_lq) into
-//        its slot of an ALL-GATHER (slots padded to a multiple of 256 rows);
+//        its slot ([32][slot rows], transposed as on one GPU) of an ALL-GATHER
+//        (slots padded to a multiple of 256 rows: a panel-QR workgroup's rows
+//        lie in one slot);
 //        every rank runs the same CholeskyQR on the gathered panel, rotated
 //        so that panel p+1's columns (the band block, on rank (p+1) mod P)
 //        come first, and finishes inline -- identical U_j, S_j everywhere;
@@ -303,14 +307,21 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 namespace {
 struct DistBlk {
     size_t bc, gat, vg, ar, total;
-    long cnt;   // rows per all-gather slot
+    long cnt;   // rows per all-gather slot, at most (the first panel)
 };
+// rows per all-gather slot for the row panel of global panel p: the most
+// trailing columns any rank holds, rounded up to a workgroup of the panel QR
+// (so every slot starts at a workgroup boundary)
+long dist_slot_rows(int n, int P, int p) {
+    int nmax = 0;
+    for (int r = 0; r < P; ++r)
+        nmax = std::max(nmax, dist_local_cols(n, 32, P, r) - dist_panels_before(p + 1, P, r) * 32);
+    return std::max(256L, ((long)nmax + 255) / 256 * 256);
+}
 DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
     const BlkLayout Ly = blk_layout(m, std::max(dist_local_cols(n, 32, P, rank), 1), elem);
-    int nmax = 0;
-    for (int r = 0; r < P; ++r) nmax = std::max(nmax, dist_local_cols(n, 32, P, r));
     DistBlk D;
-    D.cnt = std::max(256L, ((long)nmax + 255) / 256 * 256);
+    D.cnt = dist_slot_rows(n, P, 0);
     size_t off = Ly.total;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     D.bc = take((size_t)m * 32 * elem + 1032 * sizeof(double));   // V' rows, then Q_t + zero flag
@@ -348,7 +359,6 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, std::max(n_loc, 1), sizeof(T));
     const DistBlk D = dist_blk_layout(m, n, P, me, sizeof(T));
-    const long cnt = D.cnt;
     T *Lw = (T *)(ws + Ly.lw), *RwT = (T *)(ws + Ly.rwt), *Ub = (T *)(ws + Ly.ub);
     T *tf = (T *)(ws + Ly.tf);
     int *ctr = (int *)(ws + Ly.ctr);
@@ -366,7 +376,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         p.part = part; p.mp = mp; p.ksplit = ks; p.G = G; p.Tm = Tm;
         p.Qp = ws + Ly.qp; p.mq = Ly.mp;
         p.c = c; p.j = j; p.items = items; p.reduce = reduce; p.factor = factor;
-        p.sgn = sgn; p.cc = cc; p.qprow = 0; p.zfill = 0;
+        p.sgn = sgn; p.cc = cc; p.zfill = 0;
         return p;
     };
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
@@ -379,6 +389,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             const int nc = n_loc - (int)lcs;                 // local trailing columns
             T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
             double *qt = (double *)((char *)bc + (size_t)mr * 32 * sizeof(T));   // Q_t, zero flag
+            const long cnt = dist_slot_rows(n, P, p);   // <= D.cnt
             // ---- X_{j-1} (every rank) + the column panel's QR (its owner) ----------
             if (j > 0) {
                 PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1),
@@ -406,7 +417,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             T *slot = gat + (size_t)me * cnt * 32;
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
-                pa.Qp = slot; pa.qprow = 1; pa.zfill = (int)cnt;
+                pa.Qp = slot; pa.mq = cnt; pa.zfill = (int)cnt;   // [32][cnt]: coalesced, as on one GPU
                 launch_k_prep<T>(true, prep_grid(pa, target), pa, s);
                 BD_HIP(hipGetLastError());
             }
@@ -416,8 +427,9 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                                       hipMemcpyDeviceToDevice, s));
             const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
                              own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
-            BD_HIP(launch_cqr<T>(gat + (size_t)o2 * cnt * 32, 32, 1, (int)(P * cnt), Vg, 32, 1, nullptr, 0, 0, Sj,
-                                 own2 ? A + (size_t)c * lda + lcs : nullptr, 1, lda, ws, Ly, err, s, true, fl, 0));
+            BD_HIP(launch_cqr<T>(gat + (size_t)o2 * cnt * 32, 1, cnt, (int)(P * cnt), Vg, 32, 1, nullptr, 0, 0, Sj,
+                                 own2 ? A + (size_t)c * lda + lcs : nullptr, 1, lda, ws, Ly, err, s, true, fl, 0,
+                                 nullptr, cnt, cnt * 32));
             launch_dist_scatter_u<T>(Vg, (long)((me - o2 + P) % P) * cnt, nc, RwT, ldr, 128 + 32 * j, lcs, Ub, A, lda,
                                      c, own2 ? 32 : 0, s);
             // ---- X pass (local columns), partials summed and all-reduced ------------

@@ -1,6 +1,9 @@
 // Blocked stage 1: the block's delayed rank-256 update k_blkupd (gfx950).
 #include "brd_blk.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace brd {
 namespace blk {
 
@@ -107,10 +110,226 @@ __global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
             }
 }
 
+// --------------------------------------------------------------------------
+// k_blkupd_p: the same update as a persistent kernel (VERDICT r3 item 4:
+// k_blkupd loads its C tile before the K loop and stores it after, and the two
+// workgroups of a CU start in phase, so a good part of every tile had no
+// MFMA issue).  One 512-thread workgroup per CU walks tiles t = blockIdx.x,
+// + gridDim.x, ...; 8 waves of 64 x 32 (two per SIMD).  The operands reach
+// LDS by LDS-DMA (buffer_load_dwordx4 ... lds: no staging registers, rows /
+// columns past the matrix read 0), one chunk of K = 16 ahead, continuously
+// across tiles.  The accumulators start at zero; the tile's C is loaded into
+// registers during its own K loop and the previous tile's result stored
+// during it, spread over the first 8 chunks (one accumulator tile each), all
+// issued after the chunk's DMAs, so a wave's wait for its DMAs never waits
+// for C traffic (vmcnt is in order).  One register buffer holds the
+// outgoing result until its store is issued, then the incoming C.
+// --------------------------------------------------------------------------
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kGT2 = 512;
+
+template <typename T>
+struct GemmLdsP {
+    T a[2][8 * kGM * 2];    // Lw chunk [kp][row ^ kp][2] (pairs of k)
+    T b[2][kGKC * kGBP];    // RwT chunk [k][c], pitch 144
+};
+
+// 16 bytes per lane from a raw buffer (offset past num_records reads 0) into
+// LDS at lds_byte + 16 lane; counted by vmcnt, invisible to the compiler
+// (soffset: a wave-uniform byte offset added to voff)
+__device__ __forceinline__ void dma16(u32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)),
+                   "s"(__builtin_amdgcn_readfirstlane(soff))
+                 : "memory");
+}
+// raw buffer descriptor: base address, stride 0, num_records 2^31 - 1, the
+// same flags word as __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)
+__device__ __forceinline__ u32x4_t rsrc_of(const void *base) {
+    const unsigned long long p = (unsigned long long)(uintptr_t)base;
+    return u32x4_t{(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
+                   (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)), 0x7fffffffu,
+                   0x00020000u};
+}
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+template <typename T> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ void buf_st<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
+    static_assert(sizeof(T) == 8, "k_blkupd_p: fp64 (16-byte DMA granules = one k pair)");
+    typedef typename Mf<T>::v4 v4;
+    __shared__ GemmLdsP<T> L;
+    // readfirstlane: the wave index (and every DMA's LDS base) is wave-uniform, in SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = lane >> 4, l15 = lane & 15;
+    const int wr = (w >> 2) * 64, wc = (w & 3) * 32;
+    T *C = (T *)a.C;
+    const T *Lw = (const T *)a.Lw;
+    const T *RwT = (const T *)a.RwT;
+    constexpr int nc = 256 / kGKC;   // 16 chunks (K = 256)
+    constexpr int kIOC = 8;          // chunks carrying C traffic: accumulator tile (c >> 1, c & 1)
+    constexpr unsigned kOut = 0x80000000u;
+    const unsigned lds_a = (unsigned)(uintptr_t)&L.a[0][0], lds_b = (unsigned)(uintptr_t)&L.b[0][0];
+
+    // This wave's DMAs of one chunk into buffer buf: Lw instructions m = 2w,
+    // 2w+1 (kp = m >> 1, rows (m & 1) 64 + lane, stored at row ^ kp), RwT
+    // instructions k = 2w, 2w+1 (one k row of 128 columns).  Per tile two
+    // per-lane byte offsets each (kOut past the matrix), the chunk's k0 in
+    // soffset.
+    struct Dma {
+        u32x4_t ra, rb;
+        unsigned va[2], vb[2];
+    };
+    auto dma_of = [&](int t) {
+        Dma d;
+        const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
+        d.ra = rsrc_of(Lw + (size_t)r0 * 256);
+        d.rb = rsrc_of(RwT + c0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int m = 2 * w + u, kp = m >> 1, r = ((m & 1) * 64 + lane) ^ kp;
+            d.va[u] = r0 + r < a.rows ? (unsigned)((r * 256 + 2 * kp) * 8) : kOut;
+            d.vb[u] = c0 + 2 * lane < a.cols ? (unsigned)(((2 * w + u) * (int)a.ldr + 2 * lane) * 8) : kOut;
+        }
+        return d;
+    };
+    auto issue = [&](const Dma &d, int c, int buf) {
+        const int k0 = c * kGKC;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int m = 2 * w + u, kp = m >> 1;
+            dma16(d.ra, d.va[u], (unsigned)(k0 * 8),
+                  lds_a + (unsigned)((buf * 8 * kGM * 2 + (kp * kGM + (m & 1) * 64) * 2) * 8));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            dma16(d.rb, d.vb[u], (unsigned)(k0 * (int)a.ldr * 8),
+                  lds_b + (unsigned)((buf * kGKC * kGBP + (2 * w + u) * kGBP) * 8));
+    };
+    // C through raw buffer accesses relative to the tile origin; the
+    // descriptor's num_records ends at the matrix's last row (rows past it
+    // read 0 / drop), columns past it get an offset past num_records
+    struct Cio {
+        __amdgpu_buffer_rsrc_t r;
+        unsigned vb[2];
+    };
+    auto cio_of = [&](int rr0, int cc0) {
+        Cio o;
+        const unsigned long long bytes = (unsigned long long)(a.rows - rr0) * a.ldc * 8;
+        o.r = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)rr0 * a.ldc + cc0, 0,
+                                                (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int cl = wc + 16 * j + l15;
+            o.vb[j] = cc0 + cl < a.cols ? (unsigned)(((wr + q) * (int)a.ldc + cl) * 8) : kOut;
+        }
+        return o;
+    };
+    // element (i, j, g) of the lane's accumulators: row wr + 16 i + crow(q, g) (= q + 4 g)
+    auto c_at = [&](const Cio &o, int i, int j, int g) { return o.vb[j] + (unsigned)((16 * i + 4 * g) * (int)a.ldc * 8); };
+
+    v4 acc[4][2];
+    T cbuf[4][2][4];
+    bool have_prev = false;
+    Cio cprev = cio_of(0, 0);
+    Dma dnext = dma_of(blockIdx.x);
+    if (blockIdx.x < a.ntiles) issue(dnext, 0, 0);
+    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
+        const Dma dcur = dnext;
+        const Cio ccur = cio_of(r0, c0);
+        if (t + (int)gridDim.x < a.ntiles) dnext = dma_of(t + gridDim.x);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = v4{(T)0, (T)0, (T)0, (T)0};
+#pragma unroll
+        for (int c = 0; c < nc; ++c) {
+            // this chunk's DMAs (issued one chunk ago, before that chunk's C
+            // traffic: 8 VMEM ops after them in chunks 1..8, none after) landed
+            if (c >= 1 && c <= kIOC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            // the next chunk (the next tile's first after the last) into the other buffer
+            if (c + 1 < nc) issue(dcur, c + 1, (c + 1) & 1);
+            else if (t + (int)gridDim.x < a.ntiles) issue(dnext, 0, 0);
+            if (c < kIOC) {
+                const int i = c >> 1, j = c & 1;
+                if (have_prev) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(ccur.r, c_at(ccur, i, j, g));
+            }
+            const T *la = L.a[c & 1], *lb = L.b[c & 1];
+#pragma unroll
+            for (int s = 0; s < kGKC / 4; ++s) {
+                const int k = 4 * s + q, kp = k >> 1, hf = k & 1;
+                T av[4], bv[2];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) av[i] = la[2 * (kp * kGM + ((wr + 16 * i + l15) ^ kp)) + hf];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bv[j] = lb[k * kGBP + wc + 16 * j + l15];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) cbuf[i][j][g] -= acc[i][j][g];
+        have_prev = true;
+        cprev = ccur;
+    }
+    if (have_prev) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
+    }
+}
+
+static int blkupd_persistent() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("BRD_BLKUPD_P");   // A/B: 0 = the two-per-CU kernel
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
 
 template <typename T>
 void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, double by) {
-    blk_launch("s1_blkupd", fl, by, k_blkupd<T>, grid, dim3(kGT), s, g);
+    if constexpr (sizeof(T) == 8) {
+        if (blkupd_persistent()) {
+            static int cus = 0;
+            if (!cus) {
+                int dev = 0;
+                hipGetDevice(&dev);
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            }
+            const int tgt = api_overlap_active() ? api_apply_target() : cus;
+            blk_launch("s1_blkupd", fl, by, k_blkupd_p<T>, dim3(std::min<int>(g.ntiles, tgt)), dim3(kGT2), s, g);
+            return;
+        }
+    }
+    blk_launch("s1_blkupd", fl, by, k_blkupd<T>, grid, dim3(kGT), s, g);   // fp32, or BRD_BLKUPD_P=0
 }
 template void launch_k_blkupd<double>(dim3, const GemmArgs &, hipStream_t, double, double);
 template void launch_k_blkupd<float>(dim3, const GemmArgs &, hipStream_t, double, double);

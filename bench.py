@@ -188,8 +188,12 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
             "sizes_s": {str(n): round(t, 3) for n, t in pts},
             "extrapolated": {"n": gpu_n, "seconds": round(t_ext, 1),
                              "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_ext / 1e9, 4),
-                             "basis": "least-squares c*n^3 + d*n^2 (relative error) over the sampled sizes; "
-                                      "NOT measured"}}
+                             "basis": "least-squares c*n^3 + d*n^2 (relative error) over the sampled sizes "
+                                      + ",".join(str(n) for n, _ in pts) + "; NOT measured",
+                             "note": ("samples <= 1024 only: the LESS conservative fit (a 2048-inclusive "
+                                      "fit gave 2,421 s at 8192 in profiles/r02_cpu_baseline.json); "
+                                      "--cpu-n 320,640,1024,2048 adds the 2048 sample (~40 s)")
+                             if max(n for n, _ in pts) < 2048 else "2048-inclusive fit"}}
 
 
 def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):

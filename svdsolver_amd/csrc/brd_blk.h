@@ -59,6 +59,8 @@ struct RpArgs {
     const void *bsrc; long bld;     // skinny operand B (k, t) = bsrc[k*bld + t]
     int K, M;                       // S extents
     int mtiles, ksplit, kper;       // kper: k per split (multiple of 8)
+    int tiles, ns, wst;             // k_rpass_d: tiles (virtual first), 16-k stages per tile,
+                                    // stages per workgroup (linearised split)
     int nvirt;                      // ksplit if there is a virtual tile, else 0
     void *part; long mp;            // partials [ks][32][mp] (Y) / [ks][mp][32] (X)
     void *vpart;                    // virtual partials [ks][32][256] / [ks][256][32]
@@ -351,6 +353,44 @@ struct GemmArgs {
     int ntiles;                     // tiles
 };
 
+// ---- LDS-DMA and raw buffer accesses (k_blkupd_p, k_rpass_d) -----------------
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// 16 bytes per lane from a raw buffer (offset past num_records reads 0) into
+// LDS at lds_byte + 16 lane; counted by vmcnt, invisible to the compiler
+// (soffset: a wave-uniform byte offset added to voff)
+__device__ __forceinline__ void dma16(u32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)),
+                   "s"(__builtin_amdgcn_readfirstlane(soff))
+                 : "memory");
+}
+// raw buffer descriptor: base address, stride 0, num_records 2^31 - 1, the
+// same flags word as __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)
+// the same with the non-temporal policy (nt): once-read streams
+__device__ __forceinline__ void dma16_nt(u32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)),
+                   "s"(__builtin_amdgcn_readfirstlane(soff)) : "memory");
+}
+__device__ __forceinline__ u32x4_t rsrc_of(const void *base) {
+    const unsigned long long p = (unsigned long long)(uintptr_t)base;
+    return u32x4_t{(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
+                   (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)), 0x7fffffffu,
+                   0x00020000u};
+}
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+template <typename T> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ void buf_st<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
+}
+
 // ---- launches ----------------------------------------------------------------
 // Every launch of the blocked path goes through blk_launch: with brd_profile
 // on, the launch itself stamps its start and end (hipExtLaunchKernel), tagged
@@ -367,6 +407,9 @@ static inline void blk_launch(const char *kind, double flops, double bytes, F ke
 }
 
 // host launchers, one per kernel family, defined beside the kernels
+// k_rpass_d (the LDS-DMA read pass) runs this pass: fp64, no 16-byte pair
+// straddling the source's end, not disabled by BRD_RPASS_DMA=0
+bool rpass_dma_ok(bool yp, int K, int M, size_t elem);
 template <typename T>
 void launch_k_rpass(bool yp, dim3 grid, const RpArgs &a, const FinArgs &f, hipStream_t s, double fl, double by);
 template <typename T>

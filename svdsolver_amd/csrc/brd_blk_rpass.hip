@@ -2,6 +2,8 @@
 // matrix cores) and the virtual tile's partial sum k_vsum (gfx950).
 #include "brd_blk.h"
 
+#include <cstdlib>
+
 namespace brd {
 namespace blk {
 
@@ -202,8 +204,213 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
     vout[e] = s;
 }
 
+// ==========================================================================
+// k_rpass_d: the same read passes with the source stream staged through LDS
+// by LDS-DMA (k_rpass's X pass loads 16 rows x 64 B per
+// wave instruction, and both passes keep only 8 K steps of 16 B per lane in
+// flight).  Every DMA instruction moves whole >= 128-B row segments: the Y
+// pass 2 KB rows of the 256-column tile (two 1-KB instructions per row), the
+// X pass 128-B segments of 8 rows; kRS stages of 16 k (32 KB each) are in
+// flight per workgroup, with no staging registers.  The 8 waves share the K
+// stream (no K halves to reduce): wave w owns 32 of the tile's 256 m.
+//   Y: D[t][m] = sum_k B[k][t] S(k, m), S(k, m) = src[k ld + m]; LDS [k][m]
+//      (pitch 272: four k rows in distinct bank halves)
+//   X: D[m][t] = sum_k S(k, m) B[k][t], S(k, m) = src[m ld + k]; LDS [m][k]
+//      with the k pairs of row m XOR-swizzled by (m >> 1) & 7 (the DMA lane
+//      loads the pair that belongs in its slot): a half-wave's 16 rows x 16 B
+//      cover the 64 banks once
+// B (K x 32) is DMA'd beside it, [k][32], odd k rows with their halves
+// swapped (t pairs XOR 8), so rows k and k + 1 read disjoint banks.
+// Rows, columns and k past the source read 0 (offset past num_records);
+// the host uses this kernel when no 16-byte pair straddles the source's end
+// (Y: M even, X: K even -- always, for even n).
+// ==========================================================================
+constexpr int kRS = 4;      // stages in flight
+constexpr int kRK = 16;     // k per stage
+constexpr int kSY = 272;    // Y stage pitch (doubles per k row)
+struct RpLdsD {
+    double s[kRS][kRK * kSY];   // Y [k][272]; X [256][16]
+    double b[kRS][kRK * 32];
+};
+
+template <typename T, bool YP>
+__global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
+    static_assert(sizeof(T) == 8, "k_rpass_d: fp64");
+    static_assert(sizeof(FinLds) <= sizeof(RpLdsD), "cqr_finish's LDS");
+    typedef typename Mf<T>::v4 v4;
+    __shared__ RpLdsD L;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = lane >> 4, l15 = lane & 15;
+    if (a.has_fin && blockIdx.x == 0) {   // the previous panel's LU, T and R signs, beside the pass
+        cqr_finish_entry<T>(fin, tid, &L);
+        return;
+    }
+    // linearised work: the tiles' 16-k stages in a row (tile-major; the
+    // virtual tile first), wst consecutive stages per workgroup, so every
+    // workgroup streams the same bytes whatever the tile count (a workgroup
+    // crossing a tile boundary runs two segments).  The contributors of a tile
+    // write partial slots 0, 1, ... in k order; its last one zeroes the slots
+    // up to ksplit that no workgroup has (fixed-order sums stay deterministic).
+    const int g = blockIdx.x - a.has_fin;
+    const int tot = a.tiles * a.ns;
+    const int uend = min(tot, (g + 1) * a.wst);
+    constexpr unsigned kOut = 0x80000000u;
+    const unsigned lds_s = (unsigned)(uintptr_t)&L.s[0][0], lds_b = (unsigned)(uintptr_t)&L.b[0][0];
+    const T *B = (const T *)a.bsrc;
+    const int mb = 32 * w;
+    for (int u = g * a.wst; u < uend;) {
+        const int tt = u / a.ns, segend = min(uend, (tt + 1) * a.ns);
+        const bool virt = a.nvirt > 0 && tt == 0;
+        const int mx = tt - (a.nvirt > 0 ? 1 : 0);
+        const int slot = g - (tt * a.ns) / a.wst;
+        const T *S;
+        long ld;
+        int M;
+        if (virt) { S = (const T *)a.vsrc; ld = a.vld; M = kMT; }
+        else      { S = (const T *)a.src + (YP ? (long)mx * kMT : (long)mx * kMT * a.ld); ld = a.ld; M = min(kMT, a.M - mx * kMT); }
+        const int kb0 = (u - tt * a.ns) * kRK, ke0 = min(a.K, (segend - tt * a.ns) * kRK);
+        const int nst = segend - u;
+
+        // per-lane offsets relative to the stage's first k (the descriptor's
+        // base moves with the stage)
+        // Y: wave w DMAs k rows 2w, 2w+1, halves 0/1 (columns 128 h + 2 lane)
+        // X: wave w DMAs row groups 4w..4w+3 (rows 8 i + (lane >> 3), slot lane & 7)
+        // B: waves 0..3 DMA k rows 4w..4w+3 (row 4w + (lane >> 4), t pair lane & 15)
+        auto issue = [&](int st) {
+            const int k0 = kb0 + kRK * st, buf = st % kRS;
+            if constexpr (YP) {
+                const u32x4_t rs = rsrc_of(S + (long)k0 * ld);
+#pragma unroll
+                for (int uu = 0; uu < 4; ++uu) {
+                    const int kr = 2 * w + (uu >> 1), h = uu & 1, m = 128 * h + 2 * lane;
+                    const unsigned off = (k0 + kr < ke0 && m < M) ? (unsigned)((kr * (int)ld + m) * 8) : kOut;
+                    dma16(rs, off, 0, lds_s + (unsigned)((buf * kRK * kSY + kr * kSY + 128 * h) * 8));
+                }
+            } else {
+                const u32x4_t rs = rsrc_of(S + k0);
+#pragma unroll
+                for (int uu = 0; uu < 4; ++uu) {
+                    const int i = 4 * w + uu, m = 8 * i + (lane >> 3), sl = lane & 7, pr = sl ^ ((m >> 1) & 7);
+                    const unsigned off = (m < M && k0 + 2 * pr < ke0) ? (unsigned)((m * (int)ld + 2 * pr) * 8) : kOut;
+                    dma16(rs, off, 0, lds_s + (unsigned)((buf * kRK * kSY + i * 128) * 8));
+                }
+            }
+            if (w < 4) {
+                const u32x4_t rb = rsrc_of(B + (long)k0 * a.bld);
+                const int kr = 4 * w + (lane >> 4), sl = lane & 15, tp = sl ^ ((kr & 1) << 3);
+                const unsigned off = k0 + kr < ke0 ? (unsigned)((kr * (int)a.bld + 2 * tp) * 8) : kOut;
+                dma16(rb, off, 0, lds_b + (unsigned)((buf * kRK * 32 + 4 * w * 32) * 8));
+            }
+        };
+
+        v4 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = v4{(T)0, (T)0, (T)0, (T)0};
+#pragma unroll
+        for (int st = 0; st < kRS - 1; ++st)
+            if (st < nst) issue(st);
+        for (int st = 0; st < nst; ++st) {
+            // this stage's DMAs landed: the younger stages' (up to kRS - 2) may still fly
+            // (in-order vmcnt; waves 0-3 issue 5 DMAs a stage, waves 4-7 issue 4)
+            const int younger = min(nst - 1 - st, kRS - 2);
+            if (younger >= 2) {
+                if (w < 4) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+                else       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else if (younger == 1) {
+                if (w < 4) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+                else       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (st + kRS - 1 < nst) issue(st + kRS - 1);   // into the buffer every wave finished reading
+            const int buf = st % kRS;
+            const double *ls = L.s[buf], *lb = L.b[buf];
+#pragma unroll
+            for (int s4 = 0; s4 < kRK / 4; ++s4) {
+                const int k = 4 * s4 + q;
+                T bt[2], sm[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int t = 16 * h + l15;
+                    bt[h] = lb[k * 32 + 2 * ((t >> 1) ^ ((k & 1) << 3)) + (t & 1)];
+                }
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const int m = mb + 16 * p + l15;
+                    if constexpr (YP) sm[p] = ls[k * kSY + m];
+                    else sm[p] = ls[m * kRK + 2 * ((k >> 1) ^ ((m >> 1) & 7)) + (k & 1)];
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if constexpr (YP) acc[i][j] = Mf<T>::mma(bt[i], sm[j], acc[i][j]);   // [t-tile i][m-tile j]
+                        else acc[i][j] = Mf<T>::mma(sm[i], bt[j], acc[i][j]);                // [m-tile i][t-tile j]
+                    }
+            }
+        }
+        // ---- partials: slot `slot` of this tile ------------------------------
+        T *out;
+        long mp, sstride;
+        if (virt) { out = (T *)a.vpart; mp = kMT; sstride = 32L * kMT; }
+        else      { out = (T *)a.part + (size_t)mx * kMT * (YP ? 1 : 32); mp = a.mp; sstride = 32L * a.mp; }
+        T *o = out + (size_t)slot * sstride;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int r = Mf<T>::crow(q, gg);
+                    if (YP) {
+                        const int t = 16 * i + r, m = mb + 16 * j + l15;
+                        if (m < M) o[(size_t)t * mp + m] = acc[i][j][gg];
+                    } else {
+                        const int m = mb + 16 * i + r, t = 16 * j + l15;
+                        if (m < M) o[(size_t)m * 32 + t] = acc[i][j][gg];
+                    }
+                }
+        if (segend == (tt + 1) * a.ns) {   // the tile's last contributor: the unused slots read 0
+            for (int z = slot + 1; z < a.ksplit; ++z) {
+                T *oz = out + (size_t)z * sstride;
+                for (int e = tid; e < 32 * kMT; e += kRT) {
+                    const int t = e >> 8, m = e & (kMT - 1);   // (t, m) / (m, t): 32 x 256 either way
+                    if (YP) { if (m < M) oz[(size_t)t * mp + m] = (T)0; }
+                    else    { const int m2 = e >> 5, t2 = e & 31; if (m2 < M) oz[(size_t)m2 * 32 + t2] = (T)0; }
+                }
+            }
+        }
+        u = segend;
+        __syncthreads();   // every wave done with the ring before the next segment's DMAs
+    }
+}
+
+static bool rpass_dma_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("BRD_RPASS_DMA");   // A/B: 0 = the register-streaming k_rpass
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
+bool rpass_dma_ok(bool yp, int K, int M, size_t elem) {
+    // no 16-byte pair may straddle a source's end: Y tiles M wide, X rows K long
+    return elem == 8 && rpass_dma_enabled() && (yp ? M % 2 == 0 : K % 2 == 0);
+}
+
 template <typename T>
 void launch_k_rpass(bool yp, dim3 grid, const RpArgs &a, const FinArgs &f, hipStream_t s, double fl, double by) {
+    if constexpr (sizeof(T) == 8) {
+        if (a.wst > 0) {   // the host laid the split out for k_rpass_d (rpass_dma_ok)
+            if (yp) blk_launch("s1_rpass", fl, by, k_rpass_d<T, true>, grid, dim3(kRT), s, a, f);
+            else    blk_launch("s1_rpass", fl, by, k_rpass_d<T, false>, grid, dim3(kRT), s, a, f);
+            return;
+        }
+    }
     if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true, FinArgs>, grid, dim3(kRT), s, a, f);
     else    blk_launch("s1_rpass", fl, by, k_rpass<T, false, FinArgs>, grid, dim3(kRT), s, a, f);
 }

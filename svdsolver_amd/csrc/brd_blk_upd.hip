@@ -125,7 +125,6 @@ __global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
 // for C traffic (vmcnt is in order).  One register buffer holds the
 // outgoing result until its store is issued, then the incoming C.
 // --------------------------------------------------------------------------
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kGT2 = 512;
 
 template <typename T>
@@ -133,35 +132,6 @@ struct GemmLdsP {
     T a[2][8 * kGM * 2];    // Lw chunk [kp][row ^ kp][2] (pairs of k)
     T b[2][kGKC * kGBP];    // RwT chunk [k][c], pitch 144
 };
-
-// 16 bytes per lane from a raw buffer (offset past num_records reads 0) into
-// LDS at lds_byte + 16 lane; counted by vmcnt, invisible to the compiler
-// (soffset: a wave-uniform byte offset added to voff)
-__device__ __forceinline__ void dma16(u32x4_t rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)),
-                   "s"(__builtin_amdgcn_readfirstlane(soff))
-                 : "memory");
-}
-// raw buffer descriptor: base address, stride 0, num_records 2^31 - 1, the
-// same flags word as __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)
-__device__ __forceinline__ u32x4_t rsrc_of(const void *base) {
-    const unsigned long long p = (unsigned long long)(uintptr_t)base;
-    return u32x4_t{(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
-                   (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)), 0x7fffffffu,
-                   0x00020000u};
-}
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-template <typename T> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
-}
-template <typename T> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ void buf_st<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
-}
 
 template <typename T>
 __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {

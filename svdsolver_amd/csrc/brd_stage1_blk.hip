@@ -103,11 +103,31 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.mtiles = (M + kMT - 1) / kMT;
     static const int rpx = getenv("BRD_BLK_RPX") ? std::max(1, atoi(getenv("BRD_BLK_RPX"))) : 1;   // tuning
     target *= rpx;
-    int ks = std::max(1, target / std::max(1, a.mtiles + 1));
-    ks = std::min(ks, std::max(1, K / 64));
-    ks = std::min(ks, Ly.ksmax);
-    a.kper = ((K + ks - 1) / ks + 7) / 8 * 8;
-    ks = (K + a.kper - 1) / a.kper;
+    int ks, nwg;
+    a.tiles = a.ns = a.wst = 0;
+    if (rpass_dma_ok(yp, K, M, sizeof(T)) && K > 0) {
+        // k_rpass_d: the tiles' 16-k stages laid end to end and dealt in equal
+        // runs of wst stages (>= 4, i.e. >= 64 k), one run per workgroup
+        a.tiles = a.mtiles + (vsrc ? 1 : 0);
+        a.ns = (K + 15) / 16;
+        const long tot = (long)a.tiles * a.ns;
+        int wst = (int)((tot + target - 1) / std::max(1, target));
+        wst = std::max(wst, 4);
+        wst = std::max(wst, (a.ns + Ly.ksmax - 2) / (Ly.ksmax - 1));   // <= ksmax slots per tile
+        a.wst = wst;
+        nwg = (int)((tot + wst - 1) / wst);
+        ks = 1;
+        for (int t = 0; t < a.tiles; ++t)
+            ks = std::max(ks, (int)(((long)(t + 1) * a.ns - 1) / wst - ((long)t * a.ns) / wst + 1));
+        a.kper = 0;
+    } else {
+        ks = std::max(1, target / std::max(1, a.mtiles + 1));
+        ks = std::min(ks, std::max(1, K / 64));
+        ks = std::min(ks, Ly.ksmax);
+        a.kper = ((K + ks - 1) / ks + 7) / 8 * 8;
+        ks = (K + a.kper - 1) / a.kper;
+        nwg = (vsrc ? ks : 0) + a.mtiles * ks;
+    }
     a.ksplit = ks;
     a.nvirt = vsrc ? ks : 0;
     a.part = ws + Ly.part; a.mp = Ly.mp;
@@ -117,7 +137,7 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.has_fin = fin ? 1 : 0;
     const FinArgs fa = fin ? *fin : FinArgs{};
     *ksplit_out = ks;
-    dim3 grid(a.has_fin + a.nvirt + a.mtiles * ks);
+    dim3 grid(a.has_fin + nwg);
     // algorithmic: the K x M source read once, 2 x 32 flops per element
     const double fl = 2.0 * 32 * K * M, by = (double)K * M * sizeof(T);
     launch_k_rpass<T>(yp, grid, a, fa, s, fl, by);

@@ -269,8 +269,8 @@ def blkupd_roofline(bu, dtype, n):
     tf = bu["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     gbs = bu["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tn = "double" if dtype == "f64" else "float"
-    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_blkupd<" + tn)
-    return {"kernel": "k_blkupd (stage-1 delayed rank-256 trailing update, MFMA)", "bound": "mfma",
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_blkupd<" + tn, "void brd::blk::k_blkupd_p<" + tn)
+    return {"kernel": "k_blkupd / k_blkupd_p (stage-1 delayed rank-256 trailing update, MFMA)", "bound": "mfma",
             "achieved": round(tf, 3), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
             "frac": round(tf / PEAK_TFLOPS[dtype], 4),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,
@@ -289,8 +289,8 @@ def rpass_roofline(rp, dtype, n):
     gbs = rp["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tf = rp["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     tn = "double" if dtype == "f64" else "float"
-    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_rpass<" + tn)
-    return {"kernel": "k_rpass (stage-1 read passes, MFMA)", "bound": "hbm", "achieved": round(gbs, 1),
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_rpass<" + tn, "void brd::blk::k_rpass_d<" + tn)
+    return {"kernel": "k_rpass / k_rpass_d (stage-1 read passes, MFMA)", "bound": "hbm", "achieved": round(gbs, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,
             "algorithmic_bytes_per_launch": round(rp["bytes"] / launches),

@@ -460,17 +460,15 @@ static int panel_side(bool trans, T *P, long lda, const Tree &t, const TreeWs &w
 }
 
 // Blocked stage 1 (brd_stage1_blk.hip) for b = 32 -- the delayed two-sided
-// update -- over all but the last panels: the default in fp64.  In fp32 the
-// per-panel path stays the default: the blocked path's panel QR computes in
-// fp64 whatever the input type, so its latency chain costs the same while the
-// per-panel update moves half the bytes (N = 8192: stage 1 63.6 ms blocked vs
-// 59.3 per-panel; fp64 80.8 vs 86.3, 16384 fp64 366 vs 485).
+// update -- over all but the last panels: the default in both types.  Its
+// panel QR computes in fp64 whatever the input type; the read passes and the
+// block update run in the input type (fp32 N = 8192, one at a time: stage 1
+// 55.2 ms blocked vs 60.0 per-panel; fp64 72.9 vs 86.3).
 // BRD_S1_BLOCKED=1 / 0 forces either path (A/B and parity tests).
-static bool blocked_enabled(size_t elem) {
+static bool blocked_enabled(size_t) {
     const char *env = getenv("BRD_S1_BLOCKED");   // read per call: tests switch it between calls
     if (env && env[0] == '0') return false;
-    if (env && env[0] == '1') return true;
-    return elem == sizeof(double);
+    return true;
 }
 
 template <typename T>

@@ -386,7 +386,13 @@ template <typename T> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t
 template <> __device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }
+template <> __device__ __forceinline__ float buf_ld<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
 template <typename T> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ void buf_st<float>(float v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
 template <> __device__ __forceinline__ void buf_st<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
 }
@@ -407,9 +413,12 @@ static inline void blk_launch(const char *kind, double flops, double bytes, F ke
 }
 
 // host launchers, one per kernel family, defined beside the kernels
-// k_rpass_d (the LDS-DMA read pass) runs this pass: fp64, no 16-byte pair
-// straddling the source's end, not disabled by BRD_RPASS_DMA=0
-bool rpass_dma_ok(bool yp, int K, int M, size_t elem);
+// k_rpass_d (the LDS-DMA read pass) runs this pass: no 16-byte vector
+// straddling a source's end, rows 16-byte aligned, not disabled by
+// BRD_RPASS_DMA=0; its stages hold rpass_stage_k(elem) k each
+bool rpass_dma_ok(bool yp, int K, int M, size_t elem, const void *src, long ld, const void *vsrc, long vld,
+                  const void *bsrc, long bld);
+int rpass_stage_k(size_t elem);
 template <typename T>
 void launch_k_rpass(bool yp, dim3 grid, const RpArgs &a, const FinArgs &f, hipStream_t s, double fl, double by);
 template <typename T>

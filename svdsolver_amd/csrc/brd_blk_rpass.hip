@@ -226,18 +226,28 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 // (Y: M even, X: K even -- always, for even n).
 // ==========================================================================
 constexpr int kRS = 4;      // stages in flight
-constexpr int kRK = 16;     // k per stage
-constexpr int kSY = 272;    // Y stage pitch (doubles per k row)
-struct RpLdsD {
-    double s[kRS][kRK * kSY];   // Y [k][272]; X [256][16]
-    double b[kRS][kRK * 32];
+constexpr int kSY = 272;    // Y stage pitch (elements per k row: rows k..k+3 of a read in distinct banks)
+struct RpLdsD {             // 32 KB of source + 4 KB of B per stage, either type
+    double s[kRS][16 * kSY];    // Y [k][272]; X [256][kRK]
+    double b[kRS][16 * 32];     // [kRK][32]
 };
+// elements per 16-B vector, k per stage (32 KB of a 256-wide tile)
+template <typename T> constexpr int rp_epv() { return 16 / (int)sizeof(T); }
+template <typename T> constexpr int rp_krk() { return 128 / (int)sizeof(T); }
+// B's t vectors XOR-swizzled per row so the 4 k rows of a read hit distinct banks:
+// fp64 rows of 256 B (k, k + 1 in opposite halves), fp32 rows of 128 B (four rows
+// in four quarters)
+template <typename T> __device__ __forceinline__ int rp_bswz(int k) {
+    return sizeof(T) == 8 ? (k & 1) << 3 : ((k >> 1) & 1) << 2;
+}
 
 template <typename T, bool YP>
 __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
-    static_assert(sizeof(T) == 8, "k_rpass_d: fp64");
     static_assert(sizeof(FinLds) <= sizeof(RpLdsD), "cqr_finish's LDS");
     typedef typename Mf<T>::v4 v4;
+    constexpr int E = sizeof(T), EPV = rp_epv<T>(), KRK = rp_krk<T>();
+    constexpr int BVR = 32 / EPV;            // B: 16-B vectors per row
+    constexpr int BRI = 64 / BVR;            // B: rows per DMA instruction
     __shared__ RpLdsD L;
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, l15 = lane & 15;
@@ -245,7 +255,7 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
         cqr_finish_entry<T>(fin, tid, &L);
         return;
     }
-    // linearised work: the tiles' 16-k stages in a row (tile-major; the
+    // linearised work: the tiles' KRK-k stages in a row (tile-major; the
     // virtual tile first), wst consecutive stages per workgroup, so every
     // workgroup streams the same bytes whatever the tile count (a workgroup
     // crossing a tile boundary runs two segments).  The contributors of a tile
@@ -268,38 +278,42 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
         int M;
         if (virt) { S = (const T *)a.vsrc; ld = a.vld; M = kMT; }
         else      { S = (const T *)a.src + (YP ? (long)mx * kMT : (long)mx * kMT * a.ld); ld = a.ld; M = min(kMT, a.M - mx * kMT); }
-        const int kb0 = (u - tt * a.ns) * kRK, ke0 = min(a.K, (segend - tt * a.ns) * kRK);
+        const int kb0 = (u - tt * a.ns) * KRK, ke0 = min(a.K, (segend - tt * a.ns) * KRK);
         const int nst = segend - u;
 
-        // per-lane offsets relative to the stage's first k (the descriptor's
-        // base moves with the stage)
-        // Y: wave w DMAs k rows 2w, 2w+1, halves 0/1 (columns 128 h + 2 lane)
-        // X: wave w DMAs row groups 4w..4w+3 (rows 8 i + (lane >> 3), slot lane & 7)
-        // B: waves 0..3 DMA k rows 4w..4w+3 (row 4w + (lane >> 4), t pair lane & 15)
+        // Every wave issues 4 source DMAs (32 per stage) and waves 0-3 one B
+        // DMA each; per-lane offsets are relative to the stage's first k (the
+        // descriptor's base moves with the stage).
+        //   Y: instruction i = 4w + uu covers 1 KB of the stage's rows (fp64:
+        //      half a 2-KB row; fp32: a whole 1-KB row)
+        //   X: instruction i covers rows 8i..8i+7, 128 B each (lane: row
+        //      8i + lane / 8, 16-B slot lane & 7)
+        //   B: wave w's instruction covers rows BRI w .. BRI w + BRI - 1
         auto issue = [&](int st) {
-            const int k0 = kb0 + kRK * st, buf = st % kRS;
+            const int k0 = kb0 + KRK * st, buf = st % kRS;
             if constexpr (YP) {
                 const u32x4_t rs = rsrc_of(S + (long)k0 * ld);
+                constexpr int IPR = 256 * E / 1024;    // instructions per row
 #pragma unroll
                 for (int uu = 0; uu < 4; ++uu) {
-                    const int kr = 2 * w + (uu >> 1), h = uu & 1, m = 128 * h + 2 * lane;
-                    const unsigned off = (k0 + kr < ke0 && m < M) ? (unsigned)((kr * (int)ld + m) * 8) : kOut;
-                    dma16(rs, off, 0, lds_s + (unsigned)((buf * kRK * kSY + kr * kSY + 128 * h) * 8));
+                    const int i = 4 * w + uu, kr = i / IPR, h = i % IPR, m = (1024 * h + 16 * lane) / E;
+                    const unsigned off = (k0 + kr < ke0 && m < M) ? (unsigned)((kr * (int)ld + m) * E) : kOut;
+                    dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + (kr * kSY + 1024 / E * h) * E));
                 }
             } else {
                 const u32x4_t rs = rsrc_of(S + k0);
 #pragma unroll
                 for (int uu = 0; uu < 4; ++uu) {
                     const int i = 4 * w + uu, m = 8 * i + (lane >> 3), sl = lane & 7, pr = sl ^ ((m >> 1) & 7);
-                    const unsigned off = (m < M && k0 + 2 * pr < ke0) ? (unsigned)((m * (int)ld + 2 * pr) * 8) : kOut;
-                    dma16(rs, off, 0, lds_s + (unsigned)((buf * kRK * kSY + i * 128) * 8));
+                    const unsigned off = (m < M && k0 + EPV * pr < ke0) ? (unsigned)((m * (int)ld + EPV * pr) * E) : kOut;
+                    dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + i * 1024));
                 }
             }
             if (w < 4) {
                 const u32x4_t rb = rsrc_of(B + (long)k0 * a.bld);
-                const int kr = 4 * w + (lane >> 4), sl = lane & 15, tp = sl ^ ((kr & 1) << 3);
-                const unsigned off = k0 + kr < ke0 ? (unsigned)((kr * (int)a.bld + 2 * tp) * 8) : kOut;
-                dma16(rb, off, 0, lds_b + (unsigned)((buf * kRK * 32 + 4 * w * 32) * 8));
+                const int kr = BRI * w + lane / BVR, sl = lane % BVR, tp = sl ^ rp_bswz<T>(kr);
+                const unsigned off = k0 + kr < ke0 ? (unsigned)((kr * (int)a.bld + EPV * tp) * E) : kOut;
+                dma16(rb, off, 0, lds_b + (unsigned)(buf * sizeof(L.b[0]) + w * 1024));
             }
         };
 
@@ -327,21 +341,21 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
             __syncthreads();
             if (st + kRS - 1 < nst) issue(st + kRS - 1);   // into the buffer every wave finished reading
             const int buf = st % kRS;
-            const double *ls = L.s[buf], *lb = L.b[buf];
+            const T *ls = (const T *)L.s[buf], *lb = (const T *)L.b[buf];
 #pragma unroll
-            for (int s4 = 0; s4 < kRK / 4; ++s4) {
+            for (int s4 = 0; s4 < KRK / 4; ++s4) {
                 const int k = 4 * s4 + q;
                 T bt[2], sm[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int t = 16 * h + l15;
-                    bt[h] = lb[k * 32 + 2 * ((t >> 1) ^ ((k & 1) << 3)) + (t & 1)];
+                    bt[h] = lb[k * 32 + EPV * ((t / EPV) ^ rp_bswz<T>(k)) + t % EPV];
                 }
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
                     const int m = mb + 16 * p + l15;
                     if constexpr (YP) sm[p] = ls[k * kSY + m];
-                    else sm[p] = ls[m * kRK + 2 * ((k >> 1) ^ ((m >> 1) & 7)) + (k & 1)];
+                    else sm[p] = ls[m * KRK + EPV * ((k / EPV) ^ ((m >> 1) & 7)) + k % EPV];
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
@@ -377,9 +391,8 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
             for (int z = slot + 1; z < a.ksplit; ++z) {
                 T *oz = out + (size_t)z * sstride;
                 for (int e = tid; e < 32 * kMT; e += kRT) {
-                    const int t = e >> 8, m = e & (kMT - 1);   // (t, m) / (m, t): 32 x 256 either way
-                    if (YP) { if (m < M) oz[(size_t)t * mp + m] = (T)0; }
-                    else    { const int m2 = e >> 5, t2 = e & 31; if (m2 < M) oz[(size_t)m2 * 32 + t2] = (T)0; }
+                    if (YP) { const int t = e >> 8, m = e & (kMT - 1); if (m < M) oz[(size_t)t * mp + m] = (T)0; }
+                    else    { const int m = e >> 5, t = e & 31; if (m < M) oz[(size_t)m * 32 + t] = (T)0; }
                 }
             }
         }
@@ -397,19 +410,22 @@ static bool rpass_dma_enabled() {
     return v != 0;
 }
 
-bool rpass_dma_ok(bool yp, int K, int M, size_t elem) {
-    // no 16-byte pair may straddle a source's end: Y tiles M wide, X rows K long
-    return elem == 8 && rpass_dma_enabled() && (yp ? M % 2 == 0 : K % 2 == 0);
+bool rpass_dma_ok(bool yp, int K, int M, size_t elem, const void *src, long ld, const void *vsrc, long vld,
+                  const void *bsrc, long bld) {
+    // 16-byte vectors: no vector may straddle a source's end (Y tiles M wide,
+    // X rows K long) and every row must start 16-byte aligned
+    const long epv = 16 / (long)elem;
+    auto al = [&](const void *p, long l) { return p == nullptr || ((uintptr_t)p % 16 == 0 && l % epv == 0); };
+    return rpass_dma_enabled() && (yp ? M % epv == 0 : K % epv == 0) && al(src, ld) && al(vsrc, vld) && al(bsrc, bld);
 }
+int rpass_stage_k(size_t elem) { return 128 / (int)elem; }
 
 template <typename T>
 void launch_k_rpass(bool yp, dim3 grid, const RpArgs &a, const FinArgs &f, hipStream_t s, double fl, double by) {
-    if constexpr (sizeof(T) == 8) {
-        if (a.wst > 0) {   // the host laid the split out for k_rpass_d (rpass_dma_ok)
-            if (yp) blk_launch("s1_rpass", fl, by, k_rpass_d<T, true>, grid, dim3(kRT), s, a, f);
-            else    blk_launch("s1_rpass", fl, by, k_rpass_d<T, false>, grid, dim3(kRT), s, a, f);
-            return;
-        }
+    if (a.wst > 0) {   // the host laid the split out for k_rpass_d (rpass_dma_ok)
+        if (yp) blk_launch("s1_rpass", fl, by, k_rpass_d<T, true>, grid, dim3(kRT), s, a, f);
+        else    blk_launch("s1_rpass", fl, by, k_rpass_d<T, false>, grid, dim3(kRT), s, a, f);
+        return;
     }
     if (yp) blk_launch("s1_rpass", fl, by, k_rpass<T, true, FinArgs>, grid, dim3(kRT), s, a, f);
     else    blk_launch("s1_rpass", fl, by, k_rpass<T, false, FinArgs>, grid, dim3(kRT), s, a, f);

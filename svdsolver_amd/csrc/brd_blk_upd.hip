@@ -127,17 +127,22 @@ __global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
 // --------------------------------------------------------------------------
 constexpr int kGT2 = 512;
 
-template <typename T>
+// one chunk = 16 KB of Lw (128 rows) and 16 KB of RwT (128 columns): K = 16
+// fp64 / 32 fp32; a 16-B DMA granule holds EPV = 2 / 4 consecutive k of one Lw
+// row, or EPV columns of one RwT row
+template <typename T> constexpr int bu_epv() { return 16 / (int)sizeof(T); }
+template <typename T> constexpr int bu_kc() { return 128 / (int)sizeof(T); }
+template <typename T> constexpr int bu_bp() { return sizeof(T) == 8 ? kGBP : kGM; }   // RwT row pitch
 struct GemmLdsP {
-    T a[2][8 * kGM * 2];    // Lw chunk [kp][row ^ kp][2] (pairs of k)
-    T b[2][kGKC * kGBP];    // RwT chunk [k][c], pitch 144
+    double a[2][2048];      // Lw chunk [kg][row ^ kg][EPV] (granules of EPV k)
+    double b[2][kGKC * kGBP];   // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128, granules XOR 4 (k & 3)
 };
 
 template <typename T>
 __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
-    static_assert(sizeof(T) == 8, "k_blkupd_p: fp64 (16-byte DMA granules = one k pair)");
     typedef typename Mf<T>::v4 v4;
-    __shared__ GemmLdsP<T> L;
+    constexpr int E = sizeof(T), EPV = bu_epv<T>(), KC = bu_kc<T>(), BP = bu_bp<T>();
+    __shared__ GemmLdsP L;
     // readfirstlane: the wave index (and every DMA's LDS base) is wave-uniform, in SGPRs
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, l15 = lane & 15;
@@ -145,14 +150,15 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     T *C = (T *)a.C;
     const T *Lw = (const T *)a.Lw;
     const T *RwT = (const T *)a.RwT;
-    constexpr int nc = 256 / kGKC;   // 16 chunks (K = 256)
+    constexpr int nc = 256 / KC;     // chunks (K = 256): 16 fp64, 8 fp32
     constexpr int kIOC = 8;          // chunks carrying C traffic: accumulator tile (c >> 1, c & 1)
     constexpr unsigned kOut = 0x80000000u;
     const unsigned lds_a = (unsigned)(uintptr_t)&L.a[0][0], lds_b = (unsigned)(uintptr_t)&L.b[0][0];
 
     // This wave's DMAs of one chunk into buffer buf: Lw instructions m = 2w,
-    // 2w+1 (kp = m >> 1, rows (m & 1) 64 + lane, stored at row ^ kp), RwT
-    // instructions k = 2w, 2w+1 (one k row of 128 columns).  Per tile two
+    // 2w+1 (granule column kg = m >> 1, rows (m & 1) 64 + lane, stored at
+    // row ^ kg), RwT instructions i = 2w, 2w+1 (fp64: one k row of 128
+    // columns; fp32: rows 2i, 2i + 1, 32 granules each).  Per tile two
     // per-lane byte offsets each (kOut past the matrix), the chunk's k0 in
     // soffset.
     struct Dma {
@@ -166,24 +172,29 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
         d.rb = rsrc_of(RwT + c0);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int m = 2 * w + u, kp = m >> 1, r = ((m & 1) * 64 + lane) ^ kp;
-            d.va[u] = r0 + r < a.rows ? (unsigned)((r * 256 + 2 * kp) * 8) : kOut;
-            d.vb[u] = c0 + 2 * lane < a.cols ? (unsigned)(((2 * w + u) * (int)a.ldr + 2 * lane) * 8) : kOut;
+            const int m = 2 * w + u, kg = m >> 1, r = ((m & 1) * 64 + lane) ^ kg;
+            d.va[u] = r0 + r < a.rows ? (unsigned)((r * 256 + EPV * kg) * E) : kOut;
+            if constexpr (E == 8) {
+                d.vb[u] = c0 + 2 * lane < a.cols ? (unsigned)(((2 * w + u) * (int)a.ldr + 2 * lane) * 8) : kOut;
+            } else {
+                const int k = 2 * (2 * w + u) + (lane >> 5), cg = (lane & 31) ^ (4 * (k & 3));
+                d.vb[u] = c0 + 4 * cg < a.cols ? (unsigned)((k * (int)a.ldr + 4 * cg) * 4) : kOut;
+            }
         }
         return d;
     };
     auto issue = [&](const Dma &d, int c, int buf) {
-        const int k0 = c * kGKC;
+        const int k0 = c * KC;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int m = 2 * w + u, kp = m >> 1;
-            dma16(d.ra, d.va[u], (unsigned)(k0 * 8),
-                  lds_a + (unsigned)((buf * 8 * kGM * 2 + (kp * kGM + (m & 1) * 64) * 2) * 8));
+            const int m = 2 * w + u, kg = m >> 1;
+            dma16(d.ra, d.va[u], (unsigned)(k0 * E),
+                  lds_a + (unsigned)(buf * sizeof(L.a[0]) + (kg * kGM + (m & 1) * 64) * 16));
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-            dma16(d.rb, d.vb[u], (unsigned)(k0 * (int)a.ldr * 8),
-                  lds_b + (unsigned)((buf * kGKC * kGBP + (2 * w + u) * kGBP) * 8));
+            dma16(d.rb, d.vb[u], (unsigned)(k0 * (int)a.ldr * E),
+                  lds_b + (unsigned)(buf * sizeof(L.b[0]) + (2 * w + u) * (E == 8 ? kGBP * 8 : 1024)));
     };
     // C through raw buffer accesses relative to the tile origin; the
     // descriptor's num_records ends at the matrix's last row (rows past it
@@ -194,18 +205,20 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     };
     auto cio_of = [&](int rr0, int cc0) {
         Cio o;
-        const unsigned long long bytes = (unsigned long long)(a.rows - rr0) * a.ldc * 8;
+        const unsigned long long bytes = (unsigned long long)(a.rows - rr0) * a.ldc * E;
         o.r = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)rr0 * a.ldc + cc0, 0,
                                                 (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int cl = wc + 16 * j + l15;
-            o.vb[j] = cc0 + cl < a.cols ? (unsigned)(((wr + q) * (int)a.ldc + cl) * 8) : kOut;
+            o.vb[j] = cc0 + cl < a.cols ? (unsigned)(((wr + Mf<T>::crow(q, 0)) * (int)a.ldc + cl) * E) : kOut;
         }
         return o;
     };
-    // element (i, j, g) of the lane's accumulators: row wr + 16 i + crow(q, g) (= q + 4 g)
-    auto c_at = [&](const Cio &o, int i, int j, int g) { return o.vb[j] + (unsigned)((16 * i + 4 * g) * (int)a.ldc * 8); };
+    // element (i, j, g) of the lane's accumulators: row wr + 16 i + crow(q, g)
+    auto c_at = [&](const Cio &o, int i, int j, int g) {
+        return o.vb[j] + (unsigned)((16 * i + Mf<T>::crow(q, g) - Mf<T>::crow(q, 0)) * (int)a.ldc * E);
+    };
 
     v4 acc[4][2];
     T cbuf[4][2][4];
@@ -241,15 +254,19 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(ccur.r, c_at(ccur, i, j, g));
             }
-            const T *la = L.a[c & 1], *lb = L.b[c & 1];
+            const T *la = (const T *)L.a[c & 1], *lb = (const T *)L.b[c & 1];
 #pragma unroll
-            for (int s = 0; s < kGKC / 4; ++s) {
-                const int k = 4 * s + q, kp = k >> 1, hf = k & 1;
+            for (int s = 0; s < KC / 4; ++s) {
+                const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
                 T av[4], bv[2];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) av[i] = la[2 * (kp * kGM + ((wr + 16 * i + l15) ^ kp)) + hf];
+                for (int i = 0; i < 4; ++i) av[i] = la[EPV * (kg * kGM + ((wr + 16 * i + l15) ^ kg)) + he];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) bv[j] = lb[k * kGBP + wc + 16 * j + l15];
+                for (int j = 0; j < 2; ++j) {
+                    const int cl = wc + 16 * j + l15;
+                    if constexpr (E == 8) bv[j] = lb[k * BP + cl];
+                    else bv[j] = lb[k * BP + 4 * ((cl >> 2) ^ (4 * (k & 3))) + (cl & 3)];
+                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -286,8 +303,11 @@ static int blkupd_persistent() {
 
 template <typename T>
 void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, double by) {
-    if constexpr (sizeof(T) == 8) {
-        if (blkupd_persistent()) {
+    {
+        // rows 16-byte aligned for the DMA granules (fp32: ldr, 256 and the
+        // bases multiples of 4 elements)
+        const bool al = sizeof(T) == 8 || (g.ldr % 4 == 0 && (uintptr_t)g.RwT % 16 == 0 && (uintptr_t)g.Lw % 16 == 0);
+        if (blkupd_persistent() && al) {
             static int cus = 0;
             if (!cus) {
                 int dev = 0;
@@ -299,7 +319,7 @@ void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, dou
             return;
         }
     }
-    blk_launch("s1_blkupd", fl, by, k_blkupd<T>, grid, dim3(kGT), s, g);   // fp32, or BRD_BLKUPD_P=0
+    blk_launch("s1_blkupd", fl, by, k_blkupd<T>, grid, dim3(kGT), s, g);   // BRD_BLKUPD_P=0 (A/B), unaligned fp32
 }
 template void launch_k_blkupd<double>(dim3, const GemmArgs &, hipStream_t, double, double);
 template void launch_k_blkupd<float>(dim3, const GemmArgs &, hipStream_t, double, double);

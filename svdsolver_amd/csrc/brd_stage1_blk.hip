@@ -105,14 +105,15 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     target *= rpx;
     int ks, nwg;
     a.tiles = a.ns = a.wst = 0;
-    if (rpass_dma_ok(yp, K, M, sizeof(T)) && K > 0) {
-        // k_rpass_d: the tiles' 16-k stages laid end to end and dealt in equal
-        // runs of wst stages (>= 4, i.e. >= 64 k), one run per workgroup
+    if (rpass_dma_ok(yp, K, M, sizeof(T), src, ld, vsrc, vld, bsrc, bld) && K > 0) {
+        // k_rpass_d: the tiles' stages (32 KB of a 256-wide tile each) laid end
+        // to end and dealt in equal runs of wst stages, one run per workgroup
         a.tiles = a.mtiles + (vsrc ? 1 : 0);
-        a.ns = (K + 15) / 16;
+        const int krk = rpass_stage_k(sizeof(T));
+        a.ns = (K + krk - 1) / krk;
         const long tot = (long)a.tiles * a.ns;
         int wst = (int)((tot + target - 1) / std::max(1, target));
-        wst = std::max(wst, 4);
+        wst = std::max(wst, std::max(1, 64 / krk));   // >= 64 k per workgroup
         wst = std::max(wst, (a.ns + Ly.ksmax - 2) / (Ly.ksmax - 1));   // <= ksmax slots per tile
         a.wst = wst;
         nwg = (int)((tot + wst - 1) / wst);

@@ -186,19 +186,23 @@ __device__ __forceinline__ void umul_row(double (&x)[32], const double (&Ri)[32]
 // workgroup on its own, in fixed order (deterministic), scaled by the
 // per-partial powers of two scl[k]: one cluster barrier per Gram instead of a
 // slice-sum, a second barrier and a read-back.
+#ifndef BRD_GRAM_BATCH
+#define BRD_GRAM_BATCH 8    // partials per batch of loads in flight (A/B knob, tools/variant_lib.sh)
+#endif
 __device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg) {
     const int tid = threadIdx.x;
+    constexpr int GB = BRD_GRAM_BATCH;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 0; k0 < nwg; k0 += 8) {
-        double v[8][4];
+    for (int k0 = 0; k0 < nwg; k0 += GB) {
+        double v[GB][4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < GB; ++k) {
             const int kc = min(k0 + k, nwg - 1);
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[k][u] = gp[(size_t)kc * 1024 + tid + kCT * u];
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < GB; ++k) {
             const double sk = k0 + k < nwg ? scl[k0 + k] : 0.0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) acc[u] = fma(sk, v[k][u], acc[u]);

@@ -419,18 +419,19 @@ def main():
     # raised (never lowered) from whatever the environment holds (4 on the
     # MI355X pool, HIP's own default).
     if args.lanes > 1:
+        # (across GPUs every lane's stage-1 stream also carries an RCCL
+        # communicator with internal streams of its own; giving them queues
+        # too -- all 32 -- was measured slower at world size 1, N = 8192:
+        # 11.95 vs 15.30 TFLOP/s distributed and 16.9 vs 21.1 single-GPU in
+        # the same process, profiles/r04_hwq_ab.txt)
         want = min(32, 2 * args.lanes + 4)
-        # across GPUs every lane's stage-1 stream also carries an RCCL
-        # communicator, whose internal streams take hardware queues too
-        # (rocprofv3 trace at world size 1, 8 lanes: 53 streams on 20 queues,
-        # stage-2 streams sharing queues with other lanes' stage 1): all 32
-        if args.mode == "dist" and (args.force_dist or int(os.environ.get("WORLD_SIZE", "1")) > 1):
-            want = 32
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
             have = 0
-        if have < want:
+        if os.environ.get("BRD_BENCH_HWQ"):   # A/B: exactly this many (at most 32)
+            os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, int(os.environ["BRD_BENCH_HWQ"])))
+        elif have < want:
             os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     maybe_spawn(args)
     import torch

@@ -96,6 +96,15 @@ struct PrepArgs {
                               // sharded); QR the panel's first column (c; its local column)
     int zfill;                // LQ: items [items, zfill) of Qp stored as zeros (the distributed
                               // path's all-gather slot padding)
+    // gram = 1: the panel QR's first Gram partials are formed here (k_cqr_gram
+    // skipped): every workgroup's partial of its items (prescaled by its own
+    // power of two) -> gpp[wg][0, 1024), its exponent gpp[wg][1024]; the last of the workgroups
+    // covering a 256-item group (arrival counter gcnt[group], self-resetting)
+    // sums them in fixed order -> gout[group][1024], gew[group] (CqrWs gp1 /
+    // ew: what k_cqr_gram would have written)
+    int gram = 0;
+    double *gpp = nullptr, *gout = nullptr, *gew = nullptr;
+    int *gcnt = nullptr;
 };
 
 constexpr int kLG = 194;   // LQ pitches (= 2 mod 32: conflict-free A-operand reads)

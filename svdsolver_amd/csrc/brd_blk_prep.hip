@@ -1,6 +1,8 @@
 // Blocked stage 1: the per-panel corrections k_prep_lq / k_prep_qr (gfx950).
 #include "brd_blk.h"
 
+#include <climits>
+
 namespace brd {
 namespace blk {
 
@@ -24,11 +26,125 @@ namespace blk {
 // K sets are kept compact in LDS: [0, 32a) and [128, 128 + 32b) stored
 // back to back.
 // ==========================================================================
+
+// ==========================================================================
+// The panel QR's first Gram partials, formed by the prep kernel that produces
+// the panel (PrepArgs::gram): saves k_cqr_gram's launch on the chain.  Called
+// by every wave still running (nwv item waves, this one wv); fill(tw) writes
+// the wave's 16 items x 32 values (zeros past the panel) into its tile
+// tw[16][33].  tile / red overlay the kernel's K staging, free by then.  The
+// partial of the workgroup's items is prescaled by its own power of two (as
+// k_cqr_gram does per 256 rows); the last workgroup of a 256-item group to
+// arrive sums the group's partials in fixed order, rescaled to the group's
+// exponent: the same gp1 / ew k_cqr_q1 reads.  Hand-off: agent-scope
+// (L2-bypassing) stores drained before the arrival counter, agent-scope
+// loads after it.
+// ==========================================================================
+template <typename FILL>
+__device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, int ipw, double *tile, double *red,
+                                          double *smax, int *sflag, FILL &&fill) {
+    typedef Mf<double>::v4 v4d;
+    const int lane = threadIdx.x & 63, q = lane >> 4, l15 = lane & 15;
+    const int nt = 64 * nwv, tl = 64 * wv + lane;
+    __syncthreads();   // every wave is done with the K staging
+    double *tw = tile + wv * 16 * 33;
+    fill(tw);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double m = 0;
+    for (int e = lane; e < 512; e += 64) m = fmax(m, fabs(tw[(e >> 5) * 33 + (e & 31)]));
+    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (lane == 0) smax[wv] = m;
+    __syncthreads();
+    double mx = 0;
+    for (int k = 0; k < nwv; ++k) mx = fmax(mx, smax[k]);
+    int ex = INT_MIN;
+    if (mx > 0) frexp(mx, &ex);
+    const double sc = ex == INT_MIN ? 1.0 : ldexp(1.0, -ex);
+    v4d g00 = {0, 0, 0, 0}, g01 = {0, 0, 0, 0}, g11 = {0, 0, 0, 0};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+        const int k = 4 * st + q;
+        const double v0 = tw[k * 33 + l15] * sc, v1 = tw[k * 33 + 16 + l15] * sc;
+        g00 = Mf<double>::mma(v0, v0, g00);
+        g01 = Mf<double>::mma(v0, v1, g01);
+        g11 = Mf<double>::mma(v1, v1, g11);
+    }
+    for (int k = 0; k < nwv; ++k) {   // the waves' partials in fixed order
+        if (wv == k) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int rr = Mf<double>::crow(q, g);
+                if (k == 0) {
+                    red[rr * 33 + l15] = g00[g];
+                    red[rr * 33 + 16 + l15] = g01[g];
+                    red[(16 + l15) * 33 + rr] = g01[g];
+                    red[(16 + rr) * 33 + 16 + l15] = g11[g];
+                } else {
+                    red[rr * 33 + l15] += g00[g];
+                    red[rr * 33 + 16 + l15] += g01[g];
+                    red[(16 + l15) * 33 + rr] += g01[g];
+                    red[(16 + rr) * 33 + 16 + l15] += g11[g];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int wg = blockIdx.x;   // record [wg][1025]: the partial, then its exponent
+    for (int el = tl; el < 1024; el += nt)
+        __hip_atomic_store(a.gpp + (size_t)wg * 1025 + el, red[(el >> 5) * 33 + (el & 31)], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (tl == 0) __hip_atomic_store(a.gpp + (size_t)wg * 1025 + 1024, (double)ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int per = 256 / ipw, grp = wg / per, b0 = grp * per;
+    const int members = min(per, (a.items - grp * 256 + ipw - 1) / ipw);
+    if (tl == 0) {
+        const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == members - 1;
+        if (last) __hip_atomic_store(a.gcnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sflag = last;
+    }
+    __syncthreads();
+    if (!*sflag) return;
+    // one round trip: every thread loads its elements of each member's record
+    // and the members' exponents together
+    constexpr int kE = 1024 / 128;   // elements per thread (>= 2 waves)
+    double v[8][kE], ed[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const double *rec = a.gpp + (size_t)(b0 + (k < members ? k : 0)) * 1025;
+        ed[k] = __hip_atomic_load(rec + 1024, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int u = 0; u < kE; ++u) {
+            const int el = tl + nt * u;
+            v[k][u] = el < 1024 ? __hip_atomic_load(rec + el, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+    }
+    int eg = INT_MIN;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (k < members) eg = max(eg, (int)ed[k]);
+#pragma unroll
+    for (int u = 0; u < kE; ++u) {
+        const int el = tl + nt * u;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double sk = (k < members && (int)ed[k] != INT_MIN) ? ldexp(1.0, 2 * ((int)ed[k] - eg)) : 0.0;
+            acc = fma(sk, v[k][u], acc);
+        }
+        if (el < 1024) a.gout[(size_t)grp * 1024 + el] = acc;
+    }
+    if (tl == 0) a.gew[grp] = (double)eg;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
-    __shared__ T Gt[32 * kLG];   // G^T over K1 (compact)
-    __shared__ T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
+    __shared__ __attribute__((aligned(16))) T Gt[32 * kLG];   // G^T over K1 (compact)
+    __shared__ __attribute__((aligned(16))) T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
     __shared__ T Tt[32 * 34];    // T_j^T
     __shared__ T Xh[2][16][64];  // the second K half's accumulators
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -207,13 +323,25 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
             const int t = 16 * h + Mf<T>::crow(q, g);
             if (iv || il < a.zfill) QpT[(size_t)t * a.mq + il] = iv ? aq[h][g] : (T)0;
         }
+    if (a.gram) {
+        __shared__ double smax[4];
+        __shared__ int sflag;
+        prep_gram(a, a.split ? 2 : 4, wi, a.split ? kPI : 2 * kPI, reinterpret_cast<double *>(Gt),
+                  reinterpret_cast<double *>(Lt), smax, &sflag, [&](double *tw) {
+#pragma unroll
+                      for (int h = 0; h < 2; ++h)
+#pragma unroll
+                          for (int g = 0; g < 4; ++g)
+                              tw[l15 * 33 + 16 * h + Mf<T>::crow(q, g)] = iv ? (double)aq[h][g] : 0.0;
+                  });
+    }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
     typedef typename G2<T>::v2 v2;
-    __shared__ T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
+    __shared__ __attribute__((aligned(16))) T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
     __shared__ T Ss[32 * 48];        // S_{j-1}
     __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
     __shared__ T Xh[2][16][64];      // the second K half's accumulators
@@ -415,6 +543,18 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     for (int it = 0; it < 8; ++it) {
         const int t = 4 * it + q;
         if (vs) QpT[(size_t)t * a.mq + i0 + l15] = Tb[w][l15 * 34 + t];
+    }
+    if (a.gram) {
+        __shared__ double smax[4];
+        __shared__ int sflag;
+        double *st = reinterpret_cast<double *>(Gs);
+        prep_gram(a, a.split ? 2 : 4, w, a.split ? kPI : 2 * kPI, st, st + 4 * 16 * 33, smax, &sflag,
+                  [&](double *tw) {
+                      for (int e = lane; e < 512; e += 64) {
+                          const int i = e >> 5, t = e & 31;
+                          tw[i * 33 + t] = i0 + i < a.items ? (double)Tb[w][i * 34 + t] : 0.0;
+                      }
+                  });
     }
 }
 

@@ -44,7 +44,7 @@ using namespace blk;
 // device buffer: Lw m x 256, RwT 256 x ldr, partials, Qp, virtual partials
 // and result, T/S factors, cluster scratch (doubles) and counters (ints).
 struct BlkLayout {
-    size_t lw, rwt, ub, part, vpart, vout, qp, tf, cws, ctr, sg, total;
+    size_t lw, rwt, ub, part, vpart, vout, qp, tf, cws, ctr, sg, gpp, total;
     long ldr, mp;
     int ksmax, cwg;
 };
@@ -66,8 +66,10 @@ static BlkLayout blk_layout(int m, int n, size_t elem) {
     L.qp = take((size_t)32 * L.mp * elem);
     L.tf = take((size_t)8 * 1024 * elem);
     L.cws = take(cqr_ws_doubles() * sizeof(double));
-    L.ctr = take(64 * sizeof(int));
+    L.ctr = take((64 + kCW) * sizeof(int));   // counters; [64, 64 + kCW): prep Gram groups
     L.sg = take((size_t)(2 * NBMAX + 1) * 32 * sizeof(double));   // s_j per panel and side; zeros
+    // the prep kernels' Gram partials (PrepArgs::gram): per workgroup of kPI items
+    L.gpp = take((size_t)((std::max(m, n) + kPI - 1) / kPI) * 1025 * sizeof(double));
     L.total = off;
     return L;
 }
@@ -150,7 +152,7 @@ template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
                              hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr,
-                             long blk = 0, long bstride = 0) {
+                             long blk = 0, long bstride = 0, bool gram_done = false) {
     CqrArgs a;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
@@ -163,7 +165,7 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.azero = azero;
     a.qcopy = qcopy;
     a.blk = blk; a.bstride = bstride;
-    launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);
+    if (!gram_done) launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);   // else the prep kernel formed gp1 / ew
     launch_k_cqr<T>(kCqrQ1, nwg, a, fin, s);
     launch_k_cqr<T>(inl ? kCqrVInline : kCqrV, nwg, a, fin, s);
     return hipGetLastError();
@@ -180,7 +182,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     T *tf = (T *)(ws + Ly.tf);   // T_j at tf + 1024 j, S_j at tf + 1024 (4 + j)
     int *ctr = (int *)(ws + Ly.ctr);
     const long ldr = Ly.ldr;
-    hipError_t e = hipMemsetAsync(ctr, 0, 64 * sizeof(int), s);
+    hipError_t e = hipMemsetAsync(ctr, 0, (64 + kCW) * sizeof(int), s);
     if (e != hipSuccess) return e;
     double *sgq = (double *)(ws + Ly.sg), *sgl = sgq + NBMAX * 32, *sg0 = sgq + 2 * NBMAX * 32;
     e = hipMemsetAsync(sg0, 0, 32 * sizeof(double), s);   // "no correction"
@@ -198,6 +200,18 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     };
     int ks_x = 1;
     const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
+    // the prep kernels form the next panel QR's first Gram partials (no
+    // k_cqr_gram launch) unless BRD_PREP_GRAM=0 (A/B)
+    static const bool fold = !getenv("BRD_PREP_GRAM") || atoi(getenv("BRD_PREP_GRAM")) != 0;
+    auto gram_into = [&](PrepArgs &p) {
+        if (!fold) return;
+        double *cw = (double *)(ws + Ly.cws);
+        p.gram = 1;
+        p.gpp = (double *)(ws + Ly.gpp);   // records [wg][1025]
+        p.gout = cw;                    // CqrWs::gp1
+        p.gew = cw + 3072 * kCW;        // CqrWs::ew
+        p.gcnt = ctr + 64;
+    };
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
             const int c = k0 + 32 * j;
@@ -218,11 +232,12 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
                 p.cc = c; p.zfill = 0;
+                gram_into(p);
                 launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
-                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq);
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq, 1, nullptr, 0, 0, fold);
             }
             if (e != hipSuccess) return e;
             // ---- Y pass (+ the QR panel's finish) + LQ of the row panel -------
@@ -240,6 +255,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
                 p.cc = c + 32; p.zfill = 0;
+                gram_into(p);
                 launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -248,7 +264,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             const FinArgs fl = fin_of(sgl + 32 * j, Sj, A + (size_t)c * lda + c + 32, 1, lda);
             e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, n2, RwT + (size_t)(128 + 32 * j) * ldr + c + 32, 1, ldr,
                               Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s,
-                              inl, fl);
+                              inl, fl, 1, nullptr, 0, 0, fold);
             if (e != hipSuccess) return e;
             // ---- X pass (+ the LQ panel's finish) --------------------------------
             e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,

@@ -86,11 +86,15 @@ int blk_columns(int m, int n, int b) {
 
 // the prep kernels' grid: split K halves (kPI items per workgroup) while
 // that grid fits the CUs the stream may use (one workgroup per CU: LDS),
-// else 2 kPI items per workgroup, one K range per wave
+// else 2 kPI items per workgroup, one K range per wave.  Beside other work
+// (brd_set_overlap: a stream of reductions) never split: half the CUs for a
+// longer chain leaves more of the chip to the other lanes (N = 8192 fp64:
+// stream 23.8 -> 24.1 TFLOP/s; one at a time the split is worth 2.5 ms).
 static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
-    p.split = n1 <= cus ? 1 : 0;
+    static const int mode = getenv("BRD_PREP_SPLIT") ? atoi(getenv("BRD_PREP_SPLIT")) : -1;   // A/B: 0 never, 1 always
+    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !api_overlap_active())) ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 

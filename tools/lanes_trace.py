@@ -17,6 +17,9 @@ iv = [(max(s, lo), e, n) for s, e, n in iv if e > lo]
 def fam(n):
     if "band2bd" in n:
         return "stage2"
+    for k in ("k_rpass", "k_blkupd", "k_prep", "k_cqr", "k_vsum"):
+        if k in n:
+            return k
     if "k_apply_factor" in n:
         return "apply_factor"
     if "k_apply" in n:

@@ -401,13 +401,9 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
     }
 }
 
-static bool rpass_dma_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("BRD_RPASS_DMA");   // A/B: 0 = the register-streaming k_rpass
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
+static bool rpass_dma_enabled() {   // read per launch: parity tests switch it between calls
+    const char *e = getenv("BRD_RPASS_DMA");   // A/B: 0 = the register-streaming k_rpass
+    return !e || atoi(e) != 0;
 }
 
 bool rpass_dma_ok(bool yp, int K, int M, size_t elem, const void *src, long ld, const void *vsrc, long vld,

@@ -292,13 +292,9 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     }
 }
 
-static int blkupd_persistent() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("BRD_BLKUPD_P");   // A/B: 0 = the two-per-CU kernel
-        v = e ? atoi(e) : 1;
-    }
-    return v;
+static int blkupd_persistent() {   // read per launch: parity tests switch it between calls
+    const char *e = getenv("BRD_BLKUPD_P");   // A/B: 0 = the two-per-CU kernel
+    return e ? atoi(e) : 1;
 }
 
 template <typename T>

@@ -86,15 +86,16 @@ int blk_columns(int m, int n, int b) {
 
 // the prep kernels' grid: split K halves (kPI items per workgroup) while
 // that grid fits the CUs the stream may use (one workgroup per CU: LDS),
-// else 2 kPI items per workgroup, one K range per wave.  Beside other work
-// (brd_set_overlap: a stream of reductions) never split: half the CUs for a
-// longer chain leaves more of the chip to the other lanes (N = 8192 fp64:
-// stream 23.8 -> 24.1 TFLOP/s; one at a time the split is worth 2.5 ms).
+// else 2 kPI items per workgroup, one K range per wave.  (Never splitting
+// beside other work -- brd_set_overlap -- measured 23.8 -> 24.1 TFLOP/s in the
+// stream, but the two forms round the K1 sums differently, and a matrix's
+// band would then depend on whether it ran in a stream: not kept.
+// BRD_PREP_SPLIT=0 / 1 forces either form for A/B runs.)
 static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
-    static const int mode = getenv("BRD_PREP_SPLIT") ? atoi(getenv("BRD_PREP_SPLIT")) : -1;   // A/B: 0 never, 1 always
-    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !api_overlap_active())) ? 1 : 0;
+    const int mode = getenv("BRD_PREP_SPLIT") ? atoi(getenv("BRD_PREP_SPLIT")) : -1;   // A/B: 0 never, 1 always
+    p.split = mode == 0 ? 0 : (mode == 1 || n1 <= cus) ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 
@@ -206,7 +207,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
     // the prep kernels form the next panel QR's first Gram partials (no
     // k_cqr_gram launch) unless BRD_PREP_GRAM=0 (A/B)
-    static const bool fold = !getenv("BRD_PREP_GRAM") || atoi(getenv("BRD_PREP_GRAM")) != 0;
+    const bool fold = !getenv("BRD_PREP_GRAM") || atoi(getenv("BRD_PREP_GRAM")) != 0;   // read per call (tests)
     auto gram_into = [&](PrepArgs &p) {
         if (!fold) return;
         double *cw = (double *)(ws + Ly.cws);

@@ -465,6 +465,41 @@ def test_blocked_stage1_matches_per_panel(S, m, n, T):
     assert d <= (1e-13 if T == "double" else 5e-5), d
 
 
+# ---- round-4 kernels against the kernels they replaced (A/B switches) --------
+@pytest.mark.parametrize("knob", ["BRD_RPASS_DMA", "BRD_BLKUPD_P", "BRD_PREP_GRAM"])
+@pytest.mark.parametrize("m,n,T", [(1024, 1024, "double"), (1280, 1056, "double"), (1024, 1024, "float"),
+                                   (1100, 1100, "float")])
+def test_round4_kernels_match_previous(S, knob, m, n, T):
+    """The LDS-DMA read pass (k_rpass_d), the persistent block update
+    (k_blkupd_p) and the Gram partials formed in the prep kernels give the
+    same band as the kernels they replaced (knob = 0): |band| normwise fp64
+    <= 1e-13, fp32 <= 5e-5, exact zeros outside the band; each is also
+    run-to-run bitwise reproducible.  n = 1100 (fp32: not a multiple of 4)
+    takes the register-streaming read pass for the X side."""
+    import os
+    rng = np.random.default_rng(7 * m + n)
+    A = (rng.random((m, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get(knob)
+    try:
+        os.environ[knob] = "0"
+        B0 = S.brd_p1(A, 32)
+        os.environ.pop(knob, None)
+        B1 = S.brd_p1(A, 32)
+        B1b = S.brd_p1(A, 32)
+    finally:
+        if old is None:
+            os.environ.pop(knob, None)
+        else:
+            os.environ[knob] = old
+    assert np.array_equal(B1, B1b)
+    i, j = np.indices((m, n))
+    msk = (j >= i) & (j - i <= 32)
+    assert np.all(B1[~msk] == 0) and np.all(B0[~msk] == 0)
+    d = np.linalg.norm(np.abs(B1[msk].astype(np.float64)) - np.abs(B0[msk].astype(np.float64)))
+    d /= np.linalg.norm(B0[msk].astype(np.float64))
+    assert d <= (1e-13 if T == "double" else 5e-5), d
+
+
 def test_release_stream_frees_and_keeps_working(S):
     """brd_release_stream: a stream the library launched on can be released
     (drained, its workspaces and error word freed) and destroyed; a later

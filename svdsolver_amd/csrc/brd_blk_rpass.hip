@@ -225,6 +225,9 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 // the host uses this kernel when no 16-byte pair straddles the source's end
 // (Y: M even, X: K even -- always, for even n).
 // ==========================================================================
+#ifndef BRD_RPASS_HOIST
+#define BRD_RPASS_HOIST 0   // A/B knob (tools/variant_lib.sh): 1 measured no faster (X pass 110 -> 113 us)
+#endif
 constexpr int kRS = 4;      // stages in flight
 constexpr int kSY = 272;    // Y stage pitch (elements per k row: rows k..k+3 of a read in distinct banks)
 struct RpLdsD {             // 32 KB of source + 4 KB of B per stage, either type
@@ -342,28 +345,40 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
             if (st + kRS - 1 < nst) issue(st + kRS - 1);   // into the buffer every wave finished reading
             const int buf = st % kRS;
             const T *ls = (const T *)L.s[buf], *lb = (const T *)L.b[buf];
+            // every operand of the stage first (one LDS latency per stage, not
+            // one per 4-k step), then the stage's MFMAs back to back
+            // (BRD_RPASS_HOIST=1; the default is the per-step form: hoisting
+            // measured no faster, profiles/r04_rpass_variants.txt)
+            constexpr int NS4 = KRK / 4;
+            constexpr int HG = BRD_RPASS_HOIST ? NS4 : 1;   // steps per operand group
 #pragma unroll
-            for (int s4 = 0; s4 < KRK / 4; ++s4) {
-                const int k = 4 * s4 + q;
-                T bt[2], sm[2];
+            for (int s0 = 0; s0 < NS4; s0 += HG) {
+                T bt[HG][2], sm[HG][2];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int t = 16 * h + l15;
-                    bt[h] = lb[k * 32 + EPV * ((t / EPV) ^ rp_bswz<T>(k)) + t % EPV];
-                }
+                for (int u = 0; u < HG; ++u) {
+                    const int k = 4 * (s0 + u) + q;
 #pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    const int m = mb + 16 * p + l15;
-                    if constexpr (YP) sm[p] = ls[k * kSY + m];
-                    else sm[p] = ls[m * KRK + EPV * ((k / EPV) ^ ((m >> 1) & 7)) + k % EPV];
-                }
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        if constexpr (YP) acc[i][j] = Mf<T>::mma(bt[i], sm[j], acc[i][j]);   // [t-tile i][m-tile j]
-                        else acc[i][j] = Mf<T>::mma(sm[i], bt[j], acc[i][j]);                // [m-tile i][t-tile j]
+                    for (int h = 0; h < 2; ++h) {
+                        const int t = 16 * h + l15;
+                        bt[u][h] = lb[k * 32 + EPV * ((t / EPV) ^ rp_bswz<T>(k)) + t % EPV];
                     }
+#pragma unroll
+                    for (int p = 0; p < 2; ++p) {
+                        const int m = mb + 16 * p + l15;
+                        if constexpr (YP) sm[u][p] = ls[k * kSY + m];
+                        else sm[u][p] = ls[m * KRK + EPV * ((k / EPV) ^ ((m >> 1) & 7)) + k % EPV];
+                    }
+                }
+                if constexpr (BRD_RPASS_HOIST) __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead
+#pragma unroll
+                for (int u = 0; u < HG; ++u)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if constexpr (YP) acc[i][j] = Mf<T>::mma(bt[u][i], sm[u][j], acc[i][j]);   // [t-tile i][m-tile j]
+                            else acc[i][j] = Mf<T>::mma(sm[u][i], bt[u][j], acc[i][j]);                // [m-tile i][t-tile j]
+                        }
             }
         }
         // ---- partials: slot `slot` of this tile ------------------------------

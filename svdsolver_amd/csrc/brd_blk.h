@@ -77,6 +77,7 @@ constexpr int kPI = 32;    // items per workgroup when split: two item waves x t
                            // the halves meet in LDS, fixed order); unsplit: 2 kPI items,
                            // four item waves (when the split grid would exceed the CUs)
 
+constexpr int kGramRec = 1040;   // doubles per prep Gram record (1024 + exponent, 128-B lines of its own)
 struct PrepArgs {
     void *A; long lda;
     void *Lw; void *RwT; long ldr;
@@ -98,7 +99,8 @@ struct PrepArgs {
                               // path's all-gather slot padding)
     // gram = 1: the panel QR's first Gram partials are formed here (k_cqr_gram
     // skipped): every workgroup's partial of its items (prescaled by its own
-    // power of two) -> gpp[wg][0, 1024), its exponent gpp[wg][1024]; the last of the workgroups
+    // power of two) -> gpp[wg][0, 1024), its exponent gpp[wg][1024] (records
+    // kGramRec apart); the last of the workgroups
     // covering a 256-item group (arrival counter gcnt[group], self-resetting)
     // sums them in fixed order -> gout[group][1024], gew[group] (CqrWs gp1 /
     // ew: what k_cqr_gram would have written)

@@ -40,6 +40,12 @@ namespace blk {
 // (L2-bypassing) stores drained before the arrival counter, agent-scope
 // loads after it.
 // ==========================================================================
+#ifndef BRD_GRAM_LSCOPE
+#define BRD_GRAM_LSCOPE __HIP_MEMORY_SCOPE_AGENT   // A/B: the hand-off loads' scope
+#endif
+#ifndef BRD_GRAM_SSCOPE
+#define BRD_GRAM_SSCOPE __HIP_MEMORY_SCOPE_AGENT   // A/B: the hand-off stores' scope
+#endif
 template <typename FILL>
 __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, int ipw, double *tile, double *red,
                                           double *smax, int *sflag, FILL &&fill) {
@@ -91,17 +97,26 @@ __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, in
         }
         __syncthreads();
     }
-    const int wg = blockIdx.x;   // record [wg][1025]: the partial, then its exponent
+    // record [wg][kGramRec]: the partial, then its exponent.  Records start on
+    // 128-byte lines of their own: an agent-scope load may be served by this
+    // XCD's L2, which holds a line this workgroup wrote through it -- a line
+    // shared with another workgroup's record would come back with that
+    // record's part stale (seen as run-to-run differences at N = 8192).
+    const int wg = blockIdx.x;
     for (int el = tl; el < 1024; el += nt)
-        __hip_atomic_store(a.gpp + (size_t)wg * 1025 + el, red[(el >> 5) * 33 + (el & 31)], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (tl == 0) __hip_atomic_store(a.gpp + (size_t)wg * 1025 + 1024, (double)ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.gpp + (size_t)wg * kGramRec + el, red[(el >> 5) * 33 + (el & 31)], __ATOMIC_RELAXED,
+                           BRD_GRAM_SSCOPE);
+    if (tl == 0) __hip_atomic_store(a.gpp + (size_t)wg * kGramRec + 1024, (double)ex, __ATOMIC_RELAXED, BRD_GRAM_SSCOPE);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int per = 256 / ipw, grp = wg / per, b0 = grp * per;
     const int members = min(per, (a.items - grp * 256 + ipw - 1) / ipw);
     if (tl == 0) {
+#ifdef BRD_GRAM_ACQREL
+        const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#else
         const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         const int last = old == members - 1;
         if (last) __hip_atomic_store(a.gcnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *sflag = last;
@@ -114,12 +129,12 @@ __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, in
     double v[8][kE], ed[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const double *rec = a.gpp + (size_t)(b0 + (k < members ? k : 0)) * 1025;
-        ed[k] = __hip_atomic_load(rec + 1024, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double *rec = a.gpp + (size_t)(b0 + (k < members ? k : 0)) * kGramRec;
+        ed[k] = __hip_atomic_load(rec + 1024, __ATOMIC_RELAXED, BRD_GRAM_LSCOPE);
 #pragma unroll
         for (int u = 0; u < kE; ++u) {
             const int el = tl + nt * u;
-            v[k][u] = el < 1024 ? __hip_atomic_load(rec + el, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            v[k][u] = el < 1024 ? __hip_atomic_load(rec + el, __ATOMIC_RELAXED, BRD_GRAM_LSCOPE) : 0.0;
         }
     }
     int eg = INT_MIN;

@@ -69,7 +69,7 @@ static BlkLayout blk_layout(int m, int n, size_t elem) {
     L.ctr = take((64 + kCW) * sizeof(int));   // counters; [64, 64 + kCW): prep Gram groups
     L.sg = take((size_t)(2 * NBMAX + 1) * 32 * sizeof(double));   // s_j per panel and side; zeros
     // the prep kernels' Gram partials (PrepArgs::gram): per workgroup of kPI items
-    L.gpp = take((size_t)((std::max(m, n) + kPI - 1) / kPI) * 1025 * sizeof(double));
+    L.gpp = take((size_t)((std::max(m, n) + kPI - 1) / kPI) * kGramRec * sizeof(double));
     L.total = off;
     return L;
 }
@@ -207,12 +207,18 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
     // the prep kernels form the next panel QR's first Gram partials (no
     // k_cqr_gram launch) unless BRD_PREP_GRAM=0 (A/B)
-    const bool fold = !getenv("BRD_PREP_GRAM") || atoi(getenv("BRD_PREP_GRAM")) != 0;   // read per call (tests)
-    auto gram_into = [&](PrepArgs &p) {
-        if (!fold) return;
+    // (BRD_PREP_GRAM: bit 0 the QR side, bit 1 the LQ side.  Off by default:
+    // at N = 8192 about one run in twenty gives a different band from some
+    // panel on (tools/s1_repro.py; agent- and system-scope hand-offs, 128-B
+    // records, split or not: the same), cause not found; the stream gained
+    // 8 % with it, profiles/r04_prep_gram_ab.txt)
+    const int foldm = getenv("BRD_PREP_GRAM") ? atoi(getenv("BRD_PREP_GRAM")) : 0;   // read per call (tests)
+    const bool fold_qr = foldm & 1, fold_lq = foldm & 2;
+    auto gram_into = [&](PrepArgs &p, bool on) {
+        if (!on) return;
         double *cw = (double *)(ws + Ly.cws);
         p.gram = 1;
-        p.gpp = (double *)(ws + Ly.gpp);   // records [wg][1025]
+        p.gpp = (double *)(ws + Ly.gpp);   // records [wg][kGramRec]
         p.gout = cw;                    // CqrWs::gp1
         p.gew = cw + 3072 * kCW;        // CqrWs::ew
         p.gcnt = ctr + 64;
@@ -237,12 +243,12 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
                 p.cc = c; p.zfill = 0;
-                gram_into(p);
+                gram_into(p, fold_qr);
                 launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
-                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq, 1, nullptr, 0, 0, fold);
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq, 1, nullptr, 0, 0, fold_qr);
             }
             if (e != hipSuccess) return e;
             // ---- Y pass (+ the QR panel's finish) + LQ of the row panel -------
@@ -260,7 +266,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
                 p.cc = c + 32; p.zfill = 0;
-                gram_into(p);
+                gram_into(p, fold_lq);
                 launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
@@ -269,7 +275,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             const FinArgs fl = fin_of(sgl + 32 * j, Sj, A + (size_t)c * lda + c + 32, 1, lda);
             e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, n2, RwT + (size_t)(128 + 32 * j) * ldr + c + 32, 1, ldr,
                               Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s,
-                              inl, fl, 1, nullptr, 0, 0, fold);
+                              inl, fl, 1, nullptr, 0, 0, fold_lq);
             if (e != hipSuccess) return e;
             // ---- X pass (+ the LQ panel's finish) --------------------------------
             e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,

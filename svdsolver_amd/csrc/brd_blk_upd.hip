@@ -238,9 +238,18 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
         for (int c = 0; c < nc; ++c) {
             // this chunk's DMAs (issued one chunk ago, before that chunk's C
-            // traffic: 8 VMEM ops after them in chunks 1..8, none after) landed
-            if (c >= 1 && c <= kIOC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // traffic) landed: after them come 8 VMEM ops in chunks 1..8 (4
+            // stores of the previous tile, 4 loads of this one) -- only the 4
+            // loads on a workgroup's first tile, which has no previous tile
+            // (waiting for 8 there let the chunk's DMAs still be in flight:
+            // rare run-to-run differences, found by tools/s1_repro.py), none
+            // after chunk 8
+            if (c >= 1 && c <= kIOC) {
+                if (have_prev) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else           asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __syncthreads();
             // the next chunk (the next tile's first after the last) into the other buffer
             if (c + 1 < nc) issue(dcur, c + 1, (c + 1) & 1);

@@ -207,12 +207,8 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
     const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
     // the prep kernels form the next panel QR's first Gram partials (no
     // k_cqr_gram launch) unless BRD_PREP_GRAM=0 (A/B)
-    // (BRD_PREP_GRAM: bit 0 the QR side, bit 1 the LQ side.  Off by default:
-    // at N = 8192 about one run in twenty gives a different band from some
-    // panel on (tools/s1_repro.py; agent- and system-scope hand-offs, 128-B
-    // records, split or not: the same), cause not found; the stream gained
-    // 8 % with it, profiles/r04_prep_gram_ab.txt)
-    const int foldm = getenv("BRD_PREP_GRAM") ? atoi(getenv("BRD_PREP_GRAM")) : 0;   // read per call (tests)
+    // (BRD_PREP_GRAM: bit 0 the QR side, bit 1 the LQ side; default both)
+    const int foldm = getenv("BRD_PREP_GRAM") ? atoi(getenv("BRD_PREP_GRAM")) : 3;   // read per call (tests)
     const bool fold_qr = foldm & 1, fold_lq = foldm & 2;
     auto gram_into = [&](PrepArgs &p, bool on) {
         if (!on) return;

@@ -466,13 +466,13 @@ def test_blocked_stage1_matches_per_panel(S, m, n, T):
 
 
 # ---- round-4 kernels against the kernels they replaced (A/B switches) --------
-@pytest.mark.parametrize("knob", ["BRD_RPASS_DMA", "BRD_BLKUPD_P"])
+@pytest.mark.parametrize("knob", ["BRD_RPASS_DMA", "BRD_BLKUPD_P", "BRD_PREP_GRAM"])
 @pytest.mark.parametrize("m,n,T", [(1024, 1024, "double"), (1280, 1056, "double"), (1024, 1024, "float"),
                                    (1100, 1100, "float")])
 def test_round4_kernels_match_previous(S, knob, m, n, T):
-    """The LDS-DMA read pass (k_rpass_d) and the persistent block update
-    (k_blkupd_p) give the same band as the kernels they replaced (knob = 0):
-    |band| normwise fp64
+    """The LDS-DMA read pass (k_rpass_d), the persistent block update
+    (k_blkupd_p) and the Gram partials formed in the prep kernels give the
+    same band as the kernels they replaced (knob = 0): |band| normwise fp64
     <= 1e-13, fp32 <= 5e-5, exact zeros outside the band; each is also
     run-to-run bitwise reproducible.  n = 1100 (fp32: not a multiple of 4)
     takes the register-streaming read pass for the X side."""

@@ -133,10 +133,24 @@ constexpr int kGT2 = 512;
 template <typename T> constexpr int bu_epv() { return 16 / (int)sizeof(T); }
 template <typename T> constexpr int bu_kc() { return 128 / (int)sizeof(T); }
 template <typename T> constexpr int bu_bp() { return sizeof(T) == 8 ? kGBP : kGM; }   // RwT row pitch
+#ifndef BRD_BLKUPD_DEPTH
+#define BRD_BLKUPD_DEPTH 1   // chunks the DMAs run ahead (1 or 2; A/B knob: 2 measured 14.0 vs 13.8 ms)
+#endif
+constexpr int kBD = BRD_BLKUPD_DEPTH;
+constexpr int kBR = kBD == 1 ? 2 : 4;   // LDS buffers: chunk c in buffer c mod kBR (nc is a multiple)
 struct GemmLdsP {
-    double a[2][2048];      // Lw chunk [kg][row ^ kg][EPV] (granules of EPV k)
-    double b[2][kGKC * kGBP];   // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128, granules XOR 4 (k & 3)
+    double a[kBR][2048];        // Lw chunk [kg][row ^ kg][EPV] (granules of EPV k)
+    double b[kBR][kGKC * kGBP]; // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128, granules XOR 4 (k & 3)
 };
+// s_waitcnt vmcnt(n) for the few counts the block update needs (multiples of 4, <= 20)
+__device__ __forceinline__ void vmw(int n) {
+    if (n <= 0)       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n <= 4)  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n <= 8)  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n <= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n <= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else              asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+}
 
 template <typename T>
 __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
@@ -224,36 +238,55 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     T cbuf[4][2][4];
     bool have_prev = false;
     Cio cprev = cio_of(0, 0);
-    Dma dnext = dma_of(blockIdx.x);
-    if (blockIdx.x < a.ntiles) issue(dnext, 0, 0);
-    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    static_assert(nc % kBR == 0, "chunk c of every tile sits in buffer c mod kBR");
+    // DMAs run kBD chunks ahead (the next tile's first chunks during this
+    // tile's last).  Before reading chunk c a wave waits until no more VMEM
+    // ops are outstanding than it issued after chunk c's DMAs (in-order
+    // vmcnt): the later chunks' DMAs (4 each) and the C traffic of the chunks
+    // in between -- C(x) = 4 loads of this tile's C plus, when there is a
+    // previous tile (have_prev), 4 stores of its result, for x < kIOC.  (A
+    // count one tile-less first tile gets wrong lets a chunk be read before it
+    // landed: round 4 found that with tools/s1_repro.py.)
+    Dma dcur = dma_of(blockIdx.x);
+    if (blockIdx.x < a.ntiles) {
+#pragma unroll
+        for (int c = 0; c < kBD; ++c) issue(dcur, c, c);
+    }
+    int tix = 0;
+    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x, ++tix) {
         const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
-        const Dma dcur = dnext;
         const Cio ccur = cio_of(r0, c0);
-        if (t + (int)gridDim.x < a.ntiles) dnext = dma_of(t + gridDim.x);
+        const bool more = t + (int)gridDim.x < a.ntiles;
+        const Dma dnext = dma_of(more ? t + gridDim.x : t);
+        const int Cx = have_prev ? 8 : 4;                       // this tile's C ops per chunk < kIOC
+        const int Cp = tix >= 2 ? 8 : (tix == 1 ? 4 : 0);       // the previous tile's
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = v4{(T)0, (T)0, (T)0, (T)0};
 #pragma unroll
         for (int c = 0; c < nc; ++c) {
-            // this chunk's DMAs (issued one chunk ago, before that chunk's C
-            // traffic) landed: after them come 8 VMEM ops in chunks 1..8 (4
-            // stores of the previous tile, 4 loads of this one) -- only the 4
-            // loads on a workgroup's first tile, which has no previous tile
-            // (waiting for 8 there let the chunk's DMAs still be in flight:
-            // rare run-to-run differences, found by tools/s1_repro.py), none
-            // after chunk 8
-            if (c >= 1 && c <= kIOC) {
-                if (have_prev) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else           asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            {
+                // ops issued after chunk c's DMAs: C(x) of the chunks x in
+                // [c - kBD, c) (this tile's or, for x < 0, the previous tile's
+                // chunk nc + x) and the DMAs of chunks c + 1 .. c + kBD - 1
+                int n = 0;
+#pragma unroll
+                for (int x = c - kBD; x < c; ++x) {
+                    if (x >= 0) n += x < kIOC ? Cx : 0;
+                    else        n += nc + x < kIOC ? Cp : 0;
+                }
+#pragma unroll
+                for (int y = c + 1; y < c + kBD; ++y) n += (y < nc || more) ? 4 : 0;
+                vmw(n);
             }
             __syncthreads();
-            // the next chunk (the next tile's first after the last) into the other buffer
-            if (c + 1 < nc) issue(dcur, c + 1, (c + 1) & 1);
-            else if (t + (int)gridDim.x < a.ntiles) issue(dnext, 0, 0);
+            // chunk c + kBD (this tile's, or the next tile's) into the buffer read kBR - kBD chunks ago
+            {
+                const int cn = c + kBD;
+                if (cn < nc) issue(dcur, cn, cn % kBR);
+                else if (more) issue(dnext, cn - nc, (cn - nc) % kBR);
+            }
             if (c < kIOC) {
                 const int i = c >> 1, j = c & 1;
                 if (have_prev) {
@@ -263,7 +296,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(ccur.r, c_at(ccur, i, j, g));
             }
-            const T *la = (const T *)L.a[c & 1], *lb = (const T *)L.b[c & 1];
+            const T *la = (const T *)L.a[c % kBR], *lb = (const T *)L.b[c % kBR];
 #pragma unroll
             for (int s = 0; s < KC / 4; ++s) {
                 const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
@@ -290,6 +323,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
                 for (int g = 0; g < 4; ++g) cbuf[i][j][g] -= acc[i][j][g];
         have_prev = true;
         cprev = ccur;
+        dcur = dnext;
     }
     if (have_prev) {
 #pragma unroll

@@ -9,9 +9,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 import svdsolver_amd as S
 
 n = int(sys.argv[1])
+dt = torch.float32 if os.environ.get("DT") == "f32" else torch.float64
 variants = sys.argv[2].split(";") if len(sys.argv) > 2 else ["BASE=1"]
 g = torch.Generator(device="cuda"); g.manual_seed(77)
-A = torch.rand(n, n, dtype=torch.float64, device="cuda", generator=g) * 5
+A = torch.rand(n, n, dtype=dt, device="cuda", generator=g) * 5
 for v in variants:
     saved = {}
     for kv in v.split():

@@ -68,6 +68,11 @@ struct RpArgs {
     int *counter;                   // (unused)
     int *err;
     int has_fin;                    // 1: workgroup 0 runs cqr_finish of the panel the pass follows
+    int vfold = 0;                  // k_rpass_d: the virtual tile's partials summed in the pass (the
+                                    // last of its contributors to arrive, counter *counter) into vout,
+                                    // no k_vsum; the consumers patch V's / U's top block themselves
+    int va = 0, vb = 0;             // vfold: the virtual result's entries the consumer reads: k in
+                                    // [0, va) and [128, 128 + vb) (Y: G^T[t][k]; X: G[k][t])
 };
 
 // ---- k_prep_* (brd_blk_prep.hip) ---------------------------------------------
@@ -104,6 +109,9 @@ struct PrepArgs {
     // covering a 256-item group (arrival counter gcnt[group], self-resetting)
     // sums them in fixed order -> gout[group][1024], gew[group] (CqrWs gp1 /
     // ew: what k_cqr_gram would have written)
+    int vpatch = 0;           // LQ: V_j's top block as Q_t (the read pass folded k_vsum): Lt's
+                              // diagonal of V_j gets - sgn here
+    int upatch = 0;           // QR: U_{j-1}'s top block as Q_t: Rs's diagonal of U_{j-1} gets - sgn
     int gram = 0;
     double *gpp = nullptr, *gout = nullptr, *gew = nullptr;
     int *gcnt = nullptr;

@@ -218,6 +218,11 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
         T v[32];
 #pragma unroll
         for (int t = 0; t < 32; ++t) v[t] = Lw[(size_t)(c + t) * 256 + k];
+        if (a.vpatch && k >= 32 * j && k < 32 * j + 32) {   // V_j's top block: Q_t - S (what k_vsum wrote)
+#pragma unroll
+            for (int t = 0; t < 32; ++t)
+                if (k == 32 * j + t) v[t] = (T)((double)v[t] - a.sgn[t]);
+        }
 #pragma unroll
         for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
     }
@@ -415,6 +420,11 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
         T v[32];
 #pragma unroll
         for (int t = 0; t < 32; ++t) v[t] = RwT[(size_t)k * a.ldr + a.cc + t];
+        if (a.upatch && k >= 128 + 32 * jp && k < 128 + 32 * jp + 32) {   // U_{j-1}'s top block: Q_t - S
+#pragma unroll
+            for (int t = 0; t < 32; ++t)
+                if (k == 128 + 32 * jp + t) v[t] = (T)((double)v[t] - a.sgn[t]);
+        }
 #pragma unroll
         for (int t = 0; t < 32; ++t) Rs[kk * kQP + t] = -v[t];
     }

@@ -387,6 +387,7 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
         if (virt) { out = (T *)a.vpart; mp = kMT; sstride = 32L * kMT; }
         else      { out = (T *)a.part + (size_t)mx * kMT * (YP ? 1 : 32); mp = a.mp; sstride = 32L * a.mp; }
         T *o = out + (size_t)slot * sstride;
+        const bool vf = virt && a.vfold;   // hand-off below: agent-scope (L2-bypassing) stores
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -394,15 +395,70 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
 #pragma unroll
                 for (int gg = 0; gg < 4; ++gg) {
                     const int r = Mf<T>::crow(q, gg);
-                    if (YP) {
-                        const int t = 16 * i + r, m = mb + 16 * j + l15;
-                        if (m < M) o[(size_t)t * mp + m] = acc[i][j][gg];
-                    } else {
-                        const int m = mb + 16 * i + r, t = 16 * j + l15;
-                        if (m < M) o[(size_t)m * 32 + t] = acc[i][j][gg];
+                    size_t idx;
+                    bool ok;
+                    if (YP) { const int t = 16 * i + r, m = mb + 16 * j + l15; idx = (size_t)t * mp + m; ok = m < M; }
+                    else    { const int m = mb + 16 * i + r, t = 16 * j + l15; idx = (size_t)m * 32 + t; ok = m < M; }
+                    if (ok) {
+                        if (vf) __hip_atomic_store(o + idx, acc[i][j][gg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else    o[idx] = acc[i][j][gg];
                     }
                 }
-        if (segend == (tt + 1) * a.ns) {   // the tile's last contributor: the unused slots read 0
+        if (vf && a.va + a.vb > 0) {
+            // the virtual tile's contributors are workgroups 0 .. cnt0 - 1 (slots
+            // 0 .. cnt0 - 1); the last to arrive sums them in slot order into
+            // vout (what k_vsum did, without its launch on the chain) -- only
+            // the entries the consumer reads (k in [0, va) and [128, 128 + vb))
+            __shared__ int vlast;
+            const int cnt0 = (a.ns - 1) / a.wst + 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const int old = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int last = old == cnt0 - 1;
+                if (last) __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vlast = last;
+            }
+            __syncthreads();
+            if (vlast) {
+                const T *vp = (const T *)a.vpart;
+                T *vo = (T *)a.vout;
+                const int nk = a.va + a.vb, nel = 32 * nk;
+                // entry v -> its index in the [32][256] (Y) / [256][32] (X) result
+                auto at = [&](int v) {
+                    if (YP) { const int t = v / nk, kk = v - t * nk; return t * kMT + (kk < a.va ? kk : 128 + kk - a.va); }
+                    else    { const int kk = v >> 5, t = v & 31; return (kk < a.va ? kk : 128 + kk - a.va) * 32 + t; }
+                };
+#pragma unroll 1
+                for (int v0 = 0; v0 < nel; v0 += 8 * kRT) {   // 8 entries a thread per round
+                    T sum[8];
+                    int ix[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) { sum[u] = (T)0; const int v = v0 + u * kRT + tid; ix[u] = v < nel ? at(v) : -1; }
+#pragma unroll 1
+                    for (int z0 = 0; z0 < cnt0; z0 += 8) {
+                        T w[8][8];
+#pragma unroll
+                        for (int z = 0; z < 8; ++z)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u)
+                                w[z][u] = (z0 + z < cnt0 && ix[u] >= 0)
+                                              ? __hip_atomic_load(vp + (size_t)(z0 + z) * 32 * kMT + ix[u], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                              : (T)0;
+#pragma unroll
+                        for (int z = 0; z < 8; ++z)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u)
+                                if (z0 + z < cnt0) sum[u] += w[z][u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (ix[u] >= 0) vo[ix[u]] = sum[u];
+                }
+            }
+        }
+        if (segend == (tt + 1) * a.ns && !vf) {   // the tile's last contributor: the unused slots read 0
             for (int z = slot + 1; z < a.ksplit; ++z) {
                 T *oz = out + (size_t)z * sstride;
                 for (int e = tid; e < 32 * kMT; e += kRT) {

@@ -103,7 +103,8 @@ template <typename T>
 static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
                                long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
                                int target, int *ksplit_out, const FinArgs *fin, T *pbase, long pstride,
-                               const double *psgn, void *vout = nullptr) {
+                               const double *psgn, void *vout = nullptr, bool *vfolded = nullptr, int va = 0,
+                               int vb = 0) {
     RpArgs a;
     a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
     a.K = K; a.M = M;
@@ -148,8 +149,21 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     dim3 grid(a.has_fin + nwg);
     // algorithmic: the K x M source read once, 2 x 32 flops per element
     const double fl = 2.0 * 32 * K * M, by = (double)K * M * sizeof(T);
+    // the virtual tile's partials summed inside k_rpass_d (the last of its
+    // contributors to arrive; only the entries the consumer reads) when the
+    // caller's consumers patch V's / U's top block themselves (vfolded) --
+    // beside other work only (brd_set_overlap: a stream of reductions), where
+    // one fewer launch per pass is worth more than the pass's longer tail:
+    // N = 8192 fp64 stream 23.6 -> 25.0 TFLOP/s, one at a time stage 1
+    // 73.4 -> 75.6 ms.  The sum's order and the patch are k_vsum's, so the
+    // band is bitwise the same either way.  BRD_VSUM_FOLD=0 / 1 forces it.
+    const char *vfe = getenv("BRD_VSUM_FOLD");
+    const bool want = vfe ? atoi(vfe) != 0 : api_overlap_active();
+    a.vfold = (vfolded && want && a.wst > 0 && a.nvirt > 0) ? 1 : 0;
+    a.va = va; a.vb = vb;
+    if (vfolded) *vfolded = a.vfold != 0;
     launch_k_rpass<T>(yp, grid, a, fa, s, fl, by);
-    if (a.nvirt > 0) launch_k_vsum<T>((const T *)a.vpart, (T *)a.vout, a.nvirt, pbase, pstride, psgn, s);
+    if (a.nvirt > 0 && !a.vfold) launch_k_vsum<T>((const T *)a.vpart, (T *)a.vout, a.nvirt, pbase, pstride, psgn, s);
     return hipGetLastError();
 }
 
@@ -204,6 +218,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
         return f;
     };
     int ks_x = 1;
+    bool x_patch = false;          // the previous X pass left U's top block for prep_qr to patch
     const double *sg_prev = sg0;   // s of the previous LQ panel (prep_qr's correction)
     // the prep kernels form the next panel QR's first Gram partials (no
     // k_cqr_gram launch) unless BRD_PREP_GRAM=0 (A/B)
@@ -239,6 +254,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = mr; p.reduce = 1; p.factor = 1;
                 p.sgn = sg_prev;
                 p.cc = c; p.zfill = 0;
+                p.upatch = x_patch ? 1 : 0;
                 gram_into(p, fold_qr);
                 launch_k_prep<T>(false, prep_grid(p, target), p, s);
                 e = hipGetLastError();
@@ -249,9 +265,10 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             if (e != hipSuccess) return e;
             // ---- Y pass (+ the QR panel's finish) + LQ of the row panel -------
             int ks_y = 1;
+            bool yfold = false;
             e = launch_rpass<T>(true, A + (size_t)c * lda + c + 32, lda, mr, n2, Lw + (size_t)c * 256 + 32 * j, 256,
                                 Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
-                                Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j);
+                                Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j, nullptr, &yfold, 32 * j, 32 * j);
             if (e != hipSuccess) return e;
             {
                 PrepArgs p;
@@ -262,6 +279,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.c = c; p.j = j; p.items = n2; p.reduce = 0; p.factor = 0;
                 p.sgn = sgq + 32 * j;
                 p.cc = c + 32; p.zfill = 0;
+                p.vpatch = yfold ? 1 : 0;
                 gram_into(p, fold_lq);
                 launch_k_prep<T>(true, prep_grid(p, target), p, s);
                 e = hipGetLastError();
@@ -274,10 +292,13 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                               inl, fl, 1, nullptr, 0, 0, fold_lq);
             if (e != hipSuccess) return e;
             // ---- X pass (+ the LQ panel's finish) --------------------------------
+            bool xfold = false;
             e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,
                                 Ub + (size_t)(c + 32) * 32, 32, RwT + c + 32, ldr, ws, Ly, ctr + 16, err, s,
                                 target, &ks_x, inl ? nullptr : &fl,
-                                inl ? nullptr : RwT + (size_t)(128 + 32 * j) * ldr + c + 32, ldr + 1, sgl + 32 * j);
+                                inl ? nullptr : RwT + (size_t)(128 + 32 * j) * ldr + c + 32, ldr + 1, sgl + 32 * j,
+                                nullptr, &xfold, 32 * (j + 1), 32 * j);   // prep_qr(j + 1) / the block end read these
+            x_patch = !inl && xfold;   // prep_qr of the next panel patches U_j's top block
             if (e != hipSuccess) return e;
             sg_prev = inl ? sg0 : sgl + 32 * j;
         }

@@ -500,6 +500,29 @@ def test_round4_kernels_match_previous(S, knob, m, n, T):
     assert d <= (1e-13 if T == "double" else 5e-5), d
 
 
+@pytest.mark.parametrize("n,T", [(1024, "double"), (2048, "double"), (1100, "double"), (1024, "float")])
+def test_inpass_virtual_sum_bitwise(S, n, T):
+    """The read passes' virtual-tile sum done inside k_rpass_d by the last
+    contributor to arrive (BRD_VSUM_FOLD=1, the stream's default) gives the
+    band of k_vsum's separate launch (BRD_VSUM_FOLD=0, one at a time) BIT FOR
+    BIT: same slot order, same top-block patch (made by the consumer)."""
+    import os
+    rng = np.random.default_rng(11 * n)
+    A = (rng.random((n, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get("BRD_VSUM_FOLD")
+    try:
+        os.environ["BRD_VSUM_FOLD"] = "0"
+        B0 = S.brd_p1(A, 32)
+        os.environ["BRD_VSUM_FOLD"] = "1"
+        B1 = S.brd_p1(A, 32)
+    finally:
+        if old is None:
+            os.environ.pop("BRD_VSUM_FOLD", None)
+        else:
+            os.environ["BRD_VSUM_FOLD"] = old
+    assert np.array_equal(B0, B1)
+
+
 def test_release_stream_frees_and_keeps_working(S):
     """brd_release_stream: a stream the library launched on can be released
     (drained, its workspaces and error word freed) and destroyed; a later

@@ -370,6 +370,8 @@ struct GemmArgs {
     int K;                          // 256
     int tiles_c;                    // column tiles
     int ntiles;                     // tiles
+    int nfull = 0, nh = 0;          // k_blkupd_p: nh > 0: tiles [0, nfull) whole, then
+                                    // nh half tiles (64 rows) of tiles nfull, nfull + 1, ...
 };
 
 // ---- LDS-DMA and raw buffer accesses (k_blkupd_p, k_rpass_d) -----------------

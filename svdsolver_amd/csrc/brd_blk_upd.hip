@@ -140,7 +140,8 @@ constexpr int kBD = BRD_BLKUPD_DEPTH;
 constexpr int kBR = kBD == 1 ? 2 : 4;   // LDS buffers: chunk c in buffer c mod kBR (nc is a multiple)
 struct GemmLdsP {
     double a[kBR][2048];        // Lw chunk [kg][row ^ kg][EPV] (granules of EPV k)
-    double b[kBR][kGKC * kGBP]; // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128, granules XOR 4 (k & 3)
+    double b[kBR > 3 ? kBR : 3][kGKC * kGBP];   // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128,
+                                                 // granules XOR 4 (k & 3); the half tiles use three
 };
 // s_waitcnt vmcnt(n) for the few counts the block update needs (multiples of 4, <= 20)
 __device__ __forceinline__ void vmw(int n) {
@@ -217,7 +218,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
         __amdgpu_buffer_rsrc_t r;
         unsigned vb[2];
     };
-    auto cio_of = [&](int rr0, int cc0) {
+    auto cio_of = [&](int rr0, int cc0, int wrow) {
         Cio o;
         const unsigned long long bytes = (unsigned long long)(a.rows - rr0) * a.ldc * E;
         o.r = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)rr0 * a.ldc + cc0, 0,
@@ -225,7 +226,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int cl = wc + 16 * j + l15;
-            o.vb[j] = cc0 + cl < a.cols ? (unsigned)(((wr + Mf<T>::crow(q, 0)) * (int)a.ldc + cl) * E) : kOut;
+            o.vb[j] = cc0 + cl < a.cols ? (unsigned)(((wrow + Mf<T>::crow(q, 0)) * (int)a.ldc + cl) * E) : kOut;
         }
         return o;
     };
@@ -236,9 +237,31 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 
     v4 acc[4][2];
     T cbuf[4][2][4];
+    // acc += this chunk's Lw x RwT (buffer buf)
+    auto chunk_mma = [&](int buf) {
+        const T *la = (const T *)L.a[buf], *lb = (const T *)L.b[buf];
+#pragma unroll
+        for (int s = 0; s < KC / 4; ++s) {
+            const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
+            T av[4], bv[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) av[i] = la[EPV * (kg * kGM + ((wr + 16 * i + l15) ^ kg)) + he];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cl = wc + 16 * j + l15;
+                if constexpr (E == 8) bv[j] = lb[k * BP + cl];
+                else bv[j] = lb[k * BP + 4 * ((cl >> 2) ^ (4 * (k & 3))) + (cl & 3)];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
+        }
+    };
     bool have_prev = false;
-    Cio cprev = cio_of(0, 0);
+    Cio cprev = cio_of(0, 0, wr);
     static_assert(nc % kBR == 0, "chunk c of every tile sits in buffer c mod kBR");
+    static_assert(kIOC <= nc, "C traffic spread over the first kIOC chunks");
     // DMAs run kBD chunks ahead (the next tile's first chunks during this
     // tile's last).  Before reading chunk c a wave waits until no more VMEM
     // ops are outstanding than it issued after chunk c's DMAs (in-order
@@ -247,16 +270,17 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     // previous tile (have_prev), 4 stores of its result, for x < kIOC.  (A
     // count one tile-less first tile gets wrong lets a chunk be read before it
     // landed: round 4 found that with tools/s1_repro.py.)
+    const int nfull = a.nh > 0 ? a.nfull : a.ntiles;
     Dma dcur = dma_of(blockIdx.x);
-    if (blockIdx.x < a.ntiles) {
+    if (blockIdx.x < nfull) {
 #pragma unroll
         for (int c = 0; c < kBD; ++c) issue(dcur, c, c);
     }
     int tix = 0;
-    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x, ++tix) {
+    for (int t = blockIdx.x; t < nfull; t += gridDim.x, ++tix) {
         const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
-        const Cio ccur = cio_of(r0, c0);
-        const bool more = t + (int)gridDim.x < a.ntiles;
+        const Cio ccur = cio_of(r0, c0, wr);
+        const bool more = t + (int)gridDim.x < nfull;
         const Dma dnext = dma_of(more ? t + gridDim.x : t);
         const int Cx = have_prev ? 8 : 4;                       // this tile's C ops per chunk < kIOC
         const int Cp = tix >= 2 ? 8 : (tix == 1 ? 4 : 0);       // the previous tile's
@@ -296,24 +320,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(ccur.r, c_at(ccur, i, j, g));
             }
-            const T *la = (const T *)L.a[c % kBR], *lb = (const T *)L.b[c % kBR];
-#pragma unroll
-            for (int s = 0; s < KC / 4; ++s) {
-                const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
-                T av[4], bv[2];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) av[i] = la[EPV * (kg * kGM + ((wr + 16 * i + l15) ^ kg)) + he];
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int cl = wc + 16 * j + l15;
-                    if constexpr (E == 8) bv[j] = lb[k * BP + cl];
-                    else bv[j] = lb[k * BP + 4 * ((cl >> 2) ^ (4 * (k & 3))) + (cl & 3)];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
-            }
+            chunk_mma(c % kBR);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -332,6 +339,84 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
+    }
+    if (a.nh == 0) return;
+    // The last round in half tiles (launch_k_blkupd: when it holds at most
+    // half as many tiles as the grid has workgroups, e.g. every tile of the
+    // small trailing matrices): 64 x 128, eight waves of 32 x 32.  Every C
+    // element sees the same MFMA sequence as in a whole tile, so the result
+    // is bitwise the whole tile's.  A half tile's chunk is half the MFMA work
+    // of a whole one, too little to cover a chunk's DMA latency, so the DMAs
+    // run two chunks ahead through three buffers.  Items continue the whole
+    // tiles' round-robin order.
+    const int G = gridDim.x, b = blockIdx.x;
+    const int h0 = b + ((max(0, nfull - b) + G - 1) / G) * G - nfull;
+    const int wrh = (w >> 2) * 32;
+    auto chunk_mma_h = [&](int slot) {
+        const T *la = (const T *)((const char *)&L.a[0][0] + slot * 8192), *lb = (const T *)L.b[slot];
+#pragma unroll
+        for (int s = 0; s < KC / 4; ++s) {
+            const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
+            T av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = la[EPV * (kg * 64 + ((wrh + 16 * i + l15) ^ kg)) + he];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cl = wc + 16 * j + l15;
+                if constexpr (E == 8) bv[j] = lb[k * BP + cl];
+                else bv[j] = lb[k * BP + 4 * ((cl >> 2) ^ (4 * (k & 3))) + (cl & 3)];
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = Mf<T>::mma(av[i], bv[j], acc[i][j]);
+        }
+    };
+    for (int h = h0; h < a.nh; h += G) {
+        const int t = nfull + (h >> 1);
+        const int r0 = (t / a.tiles_c) * kGM + (h & 1) * 64, c0 = (t % a.tiles_c) * kGM;
+        if (r0 >= a.rows) continue;   // the lower half of a tile past the matrix (uniform)
+        // Lw: granule column kg = w of rows lane ^ kg, stored at row lane;
+        // RwT as for the whole tile
+        const u32x4_t ra = rsrc_of(Lw + (size_t)r0 * 256);
+        const unsigned vah = r0 + (lane ^ w) < a.rows ? (unsigned)(((lane ^ w) * 256 + EPV * w) * E) : kOut;
+        const Dma d = dma_of(t);
+        auto issue_h = [&](int c, int slot) {
+            const int k0 = c * KC;
+            dma16(ra, vah, (unsigned)(k0 * E), lds_a + (unsigned)(slot * 8192 + w * 64 * 16));
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                dma16(d.rb, d.vb[u], (unsigned)(k0 * (int)a.ldr * E),
+                      lds_b + (unsigned)(slot * sizeof(L.b[0]) + (2 * w + u) * (E == 8 ? kGBP * 8 : 1024)));
+        };
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = v4{(T)0, (T)0, (T)0, (T)0};
+        __syncthreads();   // every wave is done with the buffers
+        issue_h(0, 0);
+        issue_h(1, 1);
+        for (int c = 0; c < nc; ++c) {
+            // chunk c landed: only chunk c + 1's three DMAs may be younger
+            if (c + 1 < nc) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (c + 2 < nc) issue_h(c + 2, (c + 2) % 3);
+            chunk_mma_h(c % 3);
+        }
+        const Cio cc = cio_of(r0, c0, wrh);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(cc.r, c_at(cc, i, j, g));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g] - acc[i][j][g], cc.r, c_at(cc, i, j, g));
     }
 }
 
@@ -354,7 +439,19 @@ void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, dou
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             }
             const int tgt = api_overlap_active() ? api_apply_target() : cus;
-            blk_launch("s1_blkupd", fl, by, k_blkupd_p<T>, dim3(std::min<int>(g.ntiles, tgt)), dim3(kGT2), s, g);
+            // The last round in half tiles when it leaves at least half the
+            // grid idle (r = ntiles mod tgt, 2 r <= tgt; bitwise the same
+            // band).  BRD_BLKUPD_HALF=0 turns it off (A/B).
+            GemmArgs gs = g;
+            const char *he = getenv("BRD_BLKUPD_HALF");
+            const int r = g.ntiles % tgt;
+            gs.nh = 0;
+            if ((he ? atoi(he) : 1) && r > 0 && 2 * r <= tgt) {
+                gs.nfull = g.ntiles - r;
+                gs.nh = 2 * r;
+            }
+            const int items = gs.nh > 0 ? gs.nfull + gs.nh : g.ntiles;
+            blk_launch("s1_blkupd", fl, by, k_blkupd_p<T>, dim3(std::min<int>(items, tgt)), dim3(kGT2), s, gs);
             return;
         }
     }

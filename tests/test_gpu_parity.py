@@ -523,6 +523,30 @@ def test_inpass_virtual_sum_bitwise(S, n, T):
     assert np.array_equal(B0, B1)
 
 
+@pytest.mark.parametrize("m,n,T", [(1024, 1024, "double"), (1050, 1050, "double"), (1300, 1050, "double"),
+                                   (1050, 1050, "float"), (1100, 1100, "float")])
+def test_blkupd_half_tiles_bitwise(S, m, n, T):
+    """k_blkupd_p's last round in half tiles (64 x 128, BRD_BLKUPD_HALF=1,
+    the default) gives the band of whole tiles BIT FOR BIT: each C element
+    sees the same MFMA sequence.  m = 1050: the last tile row has 26 rows, so
+    its lower half lies past the matrix."""
+    import os
+    rng = np.random.default_rng(13 * m + n)
+    A = (rng.random((m, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get("BRD_BLKUPD_HALF")
+    try:
+        os.environ["BRD_BLKUPD_HALF"] = "0"
+        B0 = S.brd_p1(A, 32)
+        os.environ["BRD_BLKUPD_HALF"] = "1"
+        B1 = S.brd_p1(A, 32)
+    finally:
+        if old is None:
+            os.environ.pop("BRD_BLKUPD_HALF", None)
+        else:
+            os.environ["BRD_BLKUPD_HALF"] = old
+    assert np.array_equal(B0, B1)
+
+
 def test_release_stream_frees_and_keeps_working(S):
     """brd_release_stream: a stream the library launched on can be released
     (drained, its workspaces and error word freed) and destroyed; a later

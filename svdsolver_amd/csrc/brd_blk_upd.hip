@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(kGT, 2) k_blkupd(GemmArgs a) {
 // columns past the matrix read 0), one chunk of K = 16 ahead, continuously
 // across tiles.  The accumulators start at zero; the tile's C is loaded into
 // registers during its own K loop and the previous tile's result stored
-// during it, spread over the first 8 chunks (one accumulator tile each), all
+// during it, spread over every chunk (fp64: 2 elements each; fp32: 4), all
 // issued after the chunk's DMAs, so a wave's wait for its DMAs never waits
 // for C traffic (vmcnt is in order).  One register buffer holds the
 // outgoing result until its store is issued, then the incoming C.
@@ -143,15 +143,23 @@ struct GemmLdsP {
     double b[kBR > 3 ? kBR : 3][kGKC * kGBP];   // RwT chunk [k][c]: fp64 pitch 144; fp32 pitch 128,
                                                  // granules XOR 4 (k & 3); the half tiles use three
 };
-// s_waitcnt vmcnt(n) for the few counts the block update needs (multiples of 4, <= 20)
+// s_waitcnt vmcnt(n') for the counts the block update needs, n' <= n (rounding
+// down only ever waits for more)
 __device__ __forceinline__ void vmw(int n) {
-    if (n <= 0)       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (n <= 4)  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (n <= 8)  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n <= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (n <= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else              asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    if (n >= 20)      asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 8)  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4)  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2)  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+#ifndef BRD_BLKUPD_CSPREAD
+// C traffic over every chunk (fp64: 2 loads + 2 stores a chunk) instead of 4 +
+// 4 over the first 8: k_blkupd_p 13.29 -> 13.06 ms at N = 8192 fp64, same box,
+// bitwise the same band (profiles/r04_blkupd_half.txt).  0: the first 8 (A/B)
+#define BRD_BLKUPD_CSPREAD 1
+#endif
 
 template <typename T>
 __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
@@ -166,7 +174,8 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     const T *Lw = (const T *)a.Lw;
     const T *RwT = (const T *)a.RwT;
     constexpr int nc = 256 / KC;     // chunks (K = 256): 16 fp64, 8 fp32
-    constexpr int kIOC = 8;          // chunks carrying C traffic: accumulator tile (c >> 1, c & 1)
+    constexpr int kIOC = BRD_BLKUPD_CSPREAD ? nc : 8;   // chunks carrying C traffic
+    constexpr int EPC = 32 / kIOC;                      // accumulator elements per such chunk (flat e = 8 i + 4 j + g)
     constexpr unsigned kOut = 0x80000000u;
     const unsigned lds_a = (unsigned)(uintptr_t)&L.a[0][0], lds_b = (unsigned)(uintptr_t)&L.b[0][0];
 
@@ -266,8 +275,8 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     // tile's last).  Before reading chunk c a wave waits until no more VMEM
     // ops are outstanding than it issued after chunk c's DMAs (in-order
     // vmcnt): the later chunks' DMAs (4 each) and the C traffic of the chunks
-    // in between -- C(x) = 4 loads of this tile's C plus, when there is a
-    // previous tile (have_prev), 4 stores of its result, for x < kIOC.  (A
+    // in between -- C(x) = EPC loads of this tile's C plus, when there is a
+    // previous tile (have_prev), EPC stores of its result, for x < kIOC.  (A
     // count one tile-less first tile gets wrong lets a chunk be read before it
     // landed: round 4 found that with tools/s1_repro.py.)
     const int nfull = a.nh > 0 ? a.nfull : a.ntiles;
@@ -282,8 +291,8 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
         const Cio ccur = cio_of(r0, c0, wr);
         const bool more = t + (int)gridDim.x < nfull;
         const Dma dnext = dma_of(more ? t + gridDim.x : t);
-        const int Cx = have_prev ? 8 : 4;                       // this tile's C ops per chunk < kIOC
-        const int Cp = tix >= 2 ? 8 : (tix == 1 ? 4 : 0);       // the previous tile's
+        const int Cx = have_prev ? 2 * EPC : EPC;                         // this tile's C ops per chunk < kIOC
+        const int Cp = tix >= 2 ? 2 * EPC : (tix == 1 ? EPC : 0);         // the previous tile's
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -312,13 +321,14 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
                 else if (more) issue(dnext, cn - nc, (cn - nc) % kBR);
             }
             if (c < kIOC) {
-                const int i = c >> 1, j = c & 1;
                 if (have_prev) {
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
+                    for (int e = c * EPC; e < (c + 1) * EPC; ++e)
+                        buf_st<T>(cbuf[e >> 3][(e >> 2) & 1][e & 3], cprev.r, c_at(cprev, e >> 3, (e >> 2) & 1, e & 3));
                 }
 #pragma unroll
-                for (int g = 0; g < 4; ++g) cbuf[i][j][g] = buf_ld<T>(ccur.r, c_at(ccur, i, j, g));
+                for (int e = c * EPC; e < (c + 1) * EPC; ++e)
+                    cbuf[e >> 3][(e >> 2) & 1][e & 3] = buf_ld<T>(ccur.r, c_at(ccur, e >> 3, (e >> 2) & 1, e & 3));
             }
             chunk_mma(c % kBR);
         }

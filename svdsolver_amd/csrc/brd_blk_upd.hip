@@ -154,6 +154,12 @@ __device__ __forceinline__ void vmw(int n) {
     else if (n >= 2)  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+#ifndef BRD_BLKUPD_CAFTER
+// a chunk's C ops after its first k-step's MFMAs (the barrier's MFMA bubble
+// first): k_blkupd_p 12.98 / 12.91 -> 12.76 / 12.72 ms at N = 8192 fp64, same
+// box, bitwise the same band (profiles/r04_blkupd_half.txt).  0: before (A/B)
+#define BRD_BLKUPD_CAFTER 1
+#endif
 #ifndef BRD_BLKUPD_CSPREAD
 // C traffic over every chunk (fp64: 2 loads + 2 stores a chunk) instead of 4 +
 // 4 over the first 8: k_blkupd_p 13.29 -> 13.06 ms at N = 8192 fp64, same box,
@@ -247,10 +253,11 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     v4 acc[4][2];
     T cbuf[4][2][4];
     // acc += this chunk's Lw x RwT (buffer buf)
-    auto chunk_mma = [&](int buf) {
+    auto chunk_mma = [&](int buf, int s0 = 0, int s1 = -1) {   // k-steps [s0, s1) (-1: to the end)
         const T *la = (const T *)L.a[buf], *lb = (const T *)L.b[buf];
+        const int se = s1 < 0 ? KC / 4 : s1;
 #pragma unroll
-        for (int s = 0; s < KC / 4; ++s) {
+        for (int s = s0; s < se; ++s) {
             const int k = 4 * s + q, kg = k / EPV, he = k % EPV;
             T av[4], bv[2];
 #pragma unroll
@@ -320,6 +327,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
                 if (cn < nc) issue(dcur, cn, cn % kBR);
                 else if (more) issue(dnext, cn - nc, (cn - nc) % kBR);
             }
+            if (BRD_BLKUPD_CAFTER) chunk_mma(c % kBR, 0, 1);
             if (c < kIOC) {
                 if (have_prev) {
 #pragma unroll
@@ -330,7 +338,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
                 for (int e = c * EPC; e < (c + 1) * EPC; ++e)
                     cbuf[e >> 3][(e >> 2) & 1][e & 3] = buf_ld<T>(ccur.r, c_at(ccur, e >> 3, (e >> 2) & 1, e & 3));
             }
-            chunk_mma(c % kBR);
+            chunk_mma(c % kBR, BRD_BLKUPD_CAFTER ? 1 : 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)

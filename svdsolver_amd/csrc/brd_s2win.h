@@ -1,0 +1,229 @@
+// Stage-2 windows on the LDS ring, b = 32, fast arithmetic (the bundle
+// kernel's hot path; included by brd_stage2.hip after rsq_nr / rcp_nr /
+// fast_mod / dpp_mov).
+//
+// Reference: band_rd_right (svd_parallel.h:600) and band_rd_left (:617) --
+// a Householder reflector formed from the window's first row (right window)
+// or first column (left window), applied to the whole window only.
+//
+// Ring: band row r lives in slot r mod R; element (r, c) at
+// d[slot(r) * P + 31 + c - r] (diagonals -31 .. 2b - 1 = 63 of row r).
+//
+// W = 1: one wave per window.  Right window: lane q holds row i1 + q (32
+// elements, registers); left window: lane q holds column i1 + q.  Every lane
+// reads the source vector as an LDS broadcast and forms the reflector's
+// scalars itself, so the window is straight-line code: loads, two 32-term
+// sums (the source's squared norm and a_q . x), the scalars, the rank-1
+// update, stores.
+// W = 2: the window's rows (right) / columns (left) split over a wave pair,
+// two lanes per row / column (16 elements each), pair sums by DPP.
+#pragma once
+
+namespace brd {
+
+template <typename T>
+struct S2Ring {
+    T *d;
+    int P;           // row pitch (elements)
+    int R;           // rows
+    unsigned magic;  // ceil(2^32 / R)
+    __device__ __forceinline__ int slot(int r) const { return fast_mod(r, R, magic); }
+    // pointer p with p[c] = element (r, c)
+    __device__ __forceinline__ T *row(int r) const { return d + slot(r) * P + 31 - r; }
+};
+
+// Apply the reflector of x (x[0] the pivot, every lane holds all N) to the
+// lane's vector a (the same arithmetic for both window kinds):
+//   |x|^2 and sigma = sum_{j>=1} a_j x_j in four chains each,
+//   rn = 1/|x|, u1 = x0 - s |x|, alpha = 1/u1, tau = -s u1 / |x|,
+//   dot = a0 + alpha sigma, a0 -= tau dot, a_j -= tau dot alpha x_j.
+template <typename T, int N>
+__device__ __forceinline__ void s2_refl(T (&a)[N], const T (&x)[N]) {
+    T q0 = x[0] * x[0], q1 = (T)0, q2 = (T)0, q3 = (T)0;
+    T g0 = (T)0, g1 = (T)0, g2 = (T)0, g3 = (T)0;
+#pragma unroll
+    for (int j = 1; j < N; j += 4) {
+        q1 = fma(x[j], x[j], q1);
+        g1 = fma(a[j], x[j], g1);
+        if (j + 1 < N) { q2 = fma(x[j + 1], x[j + 1], q2); g2 = fma(a[j + 1], x[j + 1], g2); }
+        if (j + 2 < N) { q3 = fma(x[j + 2], x[j + 2], q3); g3 = fma(a[j + 2], x[j + 2], g3); }
+        if (j + 3 < N) { q0 = fma(x[j + 3], x[j + 3], q0); g0 = fma(a[j + 3], x[j + 3], g0); }
+    }
+    const T qq = (q0 + q1) + (q2 + q3);
+    const T sig = (g0 + g1) + (g2 + g3);
+    const T rn = rsq_nr(qq);
+    const T nrm = qq * rn;
+    const T sgn = x[0] >= (T)0 ? (T)-1 : (T)1;
+    const T u1 = fma(-sgn, nrm, x[0]);
+    const T alpha = rcp_nr(u1);
+    const T tau = -sgn * u1 * rn;
+    const T dot = fma(alpha, sig, a[0]);
+    const T td = tau * dot;
+    const T tda = td * alpha;
+    a[0] -= td;
+#pragma unroll
+    for (int j = 1; j < N; ++j) a[j] = fma(-tda, x[j], a[j]);
+}
+
+// Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
+// j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
+// reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
+// nc = 32 (no predicates).
+template <typename T, bool FULL>
+__device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane) {
+    constexpr int N = 32;
+    const bool rok = FULL || lane < nr;
+    const T *px = rg.row(i1) + j1;
+    T *pa = rg.row(i1 + (rok ? lane : 0)) + j1;
+    T a[N], x[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const bool cok = FULL || j < nc;
+        x[j] = cok ? px[j] : (T)0;
+        a[j] = (cok && rok) ? pa[j] : (T)0;
+    }
+    s2_refl<T, N>(a, x);
+    if (rok) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (FULL || j < nc) pa[j] = a[j];
+    }
+}
+
+// Left window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior 32 x 64 at
+// j1 = i1); the reflector comes from column j1.  Lane q holds column j1 + q.
+// Rows that do not wrap the ring sit P - 1 elements apart: one base address
+// and immediate offsets.
+template <typename T, bool FULL>
+__device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane) {
+    constexpr int N = 32;
+    const bool cok = FULL || lane < nc;
+    const int q = cok ? lane : 0;
+    const int s0 = rg.slot(i1);
+    T a[N], x[N];
+    if (s0 + N <= rg.R) {
+        T *bx = rg.d + s0 * rg.P + 31 + (j1 - i1);   // element (i1 + j, j1) at bx[j (P - 1)]
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const bool rk = FULL || j < nr;
+            x[j] = rk ? bx[j * (rg.P - 1)] : (T)0;
+            a[j] = (rk && cok) ? bx[j * (rg.P - 1) + q] : (T)0;
+        }
+        s2_refl<T, N>(a, x);
+        if (cok) {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (FULL || j < nr) bx[j * (rg.P - 1) + q] = a[j];
+        }
+    } else {
+        T *rows[N];
+        int s = s0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            rows[j] = rg.d + s * rg.P + 31 + (j1 - i1) - j;
+            s = s + 1 == rg.R ? 0 : s + 1;
+            const bool rk = FULL || j < nr;
+            x[j] = rk ? rows[j][0] : (T)0;
+            a[j] = (rk && cok) ? rows[j][q] : (T)0;
+        }
+        s2_refl<T, N>(a, x);
+        if (cok) {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (FULL || j < nr) rows[j][q] = a[j];
+        }
+    }
+}
+
+// ---- wave pair (W = 2) ------------------------------------------------------
+// The pair's waves meet on the source vector: wave 1 raises its flag once it
+// has read the source; wave 0 (which holds the source row / column) stores
+// only after that.
+struct S2Pair {
+    int *xr;   // two flag words
+    int pw;    // 0 or 1
+    int tag;
+    __device__ __forceinline__ void read_done(int lane) const {
+        if (pw == 0) return;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(xr + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void before_store() const {
+        if (pw != 0) return;
+        for (int spin = 0; spin < (1 << 22); ++spin) {
+            if (__hip_atomic_load(xr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= tag) break;
+            __builtin_amdgcn_s_sleep(0);
+        }
+    }
+};
+
+template <typename T, int N>
+__device__ __forceinline__ void s2_refl_pair(T (&a)[N], const T (&x)[N], T x0, bool piv) {
+    T q0 = (T)0, q1 = (T)0, g0 = (T)0, g1 = (T)0;
+#pragma unroll
+    for (int k = 0; k < N; k += 2) {
+        q0 = fma(x[k], x[k], q0);
+        q1 = fma(x[k + 1], x[k + 1], q1);
+        if (k > 0 || !piv) g0 = fma(a[k], x[k], g0);
+        g1 = fma(a[k + 1], x[k + 1], g1);
+    }
+    const T qq = group_sum<2>(q0 + q1);
+    const T rn = rsq_nr(qq);
+    const T nrm = qq * rn;
+    const T sgn = x0 >= (T)0 ? (T)-1 : (T)1;
+    const T u1 = fma(-sgn, nrm, x0);
+    const T alpha = rcp_nr(u1);
+    const T tau = -sgn * u1 * rn;
+    const T dot = group_sum<2>(fma(alpha, g0 + g1, piv ? a[0] : (T)0));
+    const T td = tau * dot;
+    const T tda = td * alpha;
+    const T e0 = piv ? a[0] - td : fma(-tda, x[0], a[0]);
+#pragma unroll
+    for (int k = 1; k < N; ++k) a[k] = fma(-tda, x[k], a[k]);
+    a[0] = e0;
+}
+
+// right window, interior only (64 x 32): lane L = 64 pw + lane -> row L / 2,
+// elements 16 (L % 2) + [0, 16)
+template <typename T, bool FULL>
+__device__ __forceinline__ void s2_right_w2(const S2Ring<T> &rg, int i1, int nr, int nc, int lane, const S2Pair &pr) {
+    constexpr int E = 16;
+    const int L = 64 * pr.pw + lane, h = L & 1, r = L >> 1;
+    const T *px = rg.row(i1) + i1 + 32 + E * h;
+    T *pa = rg.row(i1 + r) + i1 + 32 + E * h;
+    T a[E], x[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) { x[k] = px[k]; a[k] = pa[k]; }
+    const T x0 = rg.row(i1)[i1 + 32];
+    pr.read_done(lane);
+    s2_refl_pair<T, E>(a, x, x0, h == 0);
+    pr.before_store();
+#pragma unroll
+    for (int k = 0; k < E; ++k) pa[k] = a[k];
+}
+
+// left window, interior only (32 x 64): lane L -> column L / 2, rows 16 (L % 2) + [0, 16)
+template <typename T, bool FULL>
+__device__ __forceinline__ void s2_left_w2(const S2Ring<T> &rg, int i1, int nr, int nc, int lane, const S2Pair &pr) {
+    constexpr int E = 16;
+    const int L = 64 * pr.pw + lane, h = L & 1, c = L >> 1;
+    const int s0 = rg.slot(i1 + E * h);
+    T a[E], x[E];
+    T *rows[E];
+    int s = s0;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        rows[k] = rg.d + s * rg.P + 31 - (E * h + k);
+        s = s + 1 == rg.R ? 0 : s + 1;
+        x[k] = rows[k][0];
+        a[k] = rows[k][c];
+    }
+    const T x0 = rg.row(i1)[i1];
+    pr.read_done(lane);
+    s2_refl_pair<T, E>(a, x, x0, h == 0);
+    pr.before_store();
+#pragma unroll
+    for (int k = 0; k < E; ++k) rows[k][c] = a[k];
+}
+
+}  // namespace brd

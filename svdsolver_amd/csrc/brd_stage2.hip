@@ -1176,6 +1176,366 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
     }
 }
 
+}  // namespace brd
+#include "brd_s2win.h"
+namespace brd {
+
+// ==========================================================================
+// k_sweeps: the b = 32 fast-arithmetic bundle kernel (the production stage 2).
+// Workgroup = S compute waves (one wave per sweep, brd_s2win.h windows) +
+// loader + writer + poller; bundle beta = sweeps beta*S .. beta*S+S-1, dealt
+// round-robin to a persistent grid, rows handed between bundles through HBM
+// exactly as in k_band2bd_bundle (sc1 stores drained before an sc1 flag,
+// sc1 polls, LDS-DMA loads).  What differs from k_band2bd_bundle:
+//  * one wave per window (no per-task meeting of a wave pair; the window is
+//    straight-line code on 32 elements per lane);
+//  * the progress words are plain LDS stores behind the window's ring stores
+//    (LDS executes a wave's operations in order), no lgkmcnt drain on the
+//    compute waves' critical path;
+//  * the writer publishes rows_done per 8-row piece behind counted vmcnt
+//    waits, so the next bundle's loader starts on the first piece while the
+//    rest drains;
+//  * a compact role split (no SGPR spills: one window code path per kind).
+// ==========================================================================
+constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
+struct SweepFlags {
+    int prog[12];    // tasks completed per compute wave
+    int front[12];   // top row of each compute wave's next window (n when done)
+    int loaded;      // rows < loaded are in the ring (loader wave)
+    int freed;       // ring slots of rows < freed may be reused (writer waves, in row order)
+    int avail;       // rows < avail have been written back by bundle beta-1 (poller wave)
+    int wturn;       // writers: index of the next batch to claim
+    int wclaim;      // writers: first row of the next batch
+    int wpub;        // writers: rows < wpub published in rows_done[beta] (in row order)
+};
+
+#ifdef BRD_S2TRACE
+// Diagnostic build only (tools/s2trace.py): per-task and per-publication
+// timeline of bundles kTrB0 .. kTrB0 + kTrNB - 1 on the chip-wide 100 MHz clock.
+constexpr int kTrB0 = 600, kTrNB = 4, kTrTasks = 600, kTrPub = 1024;
+struct S2Trace {
+    unsigned long long task[kTrNB][12][kTrTasks][4];   // start, lag done, rows ready, end
+    unsigned long long pub[kTrNB][8][kTrPub][2];       // loader / writer / poller / claim / issued / ldissue / freed
+    int npub[kTrNB][8];
+    unsigned long long bundle[kTrNB][4];               // start, end, block, xcc
+};
+__device__ S2Trace g_s2tr;
+#define TRB(beta) ((beta) >= kTrB0 && (beta) < kTrB0 + kTrNB)
+#define TRT(beta, w, t, k)                                                                      \
+    do {                                                                                        \
+        if (TRB(beta) && (t) < kTrTasks && lane == 0)                                           \
+            g_s2tr.task[(beta) - kTrB0][w][t][k] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#define TRP(beta, kind, val)                                                                    \
+    do {                                                                                        \
+        if (TRB(beta) && lane == 0) {                                                           \
+            const int q_ = g_s2tr.npub[(beta) - kTrB0][kind]++;                                 \
+            if (q_ < kTrPub) {                                                                  \
+                g_s2tr.pub[(beta) - kTrB0][kind][q_][0] = __builtin_amdgcn_s_memrealtime();     \
+                g_s2tr.pub[(beta) - kTrB0][kind][q_][1] = (val);                                \
+            }                                                                                   \
+        }                                                                                       \
+    } while (0)
+#else
+#define TRT(beta, w, t, k) do {} while (0)
+#define TRP(beta, kind, val) do {} while (0)
+#endif
+
+template <typename T> constexpr int sweeps_max_threads() { return sizeof(T) == 8 ? 512 : 768; }
+
+__device__ __forceinline__ int lds_ld(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(sweeps_max_threads<T>())
+k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
+{
+    constexpr int b = 32;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int P = ring_pitch<T>(b);
+    T *ring = (T *)smem;
+    const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
+    SweepFlags *F = (SweepFlags *)(smem + ring_bytes);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const S2Ring<T> rg{ring, P, R, magic};
+    const int nbundles = (n - 1 + S - 1) / S;
+
+    for (int beta = blockIdx.x; beta < nbundles; beta += gridDim.x) {
+        const int i0 = beta * S;
+        const int nsw = min(S, n - 1 - i0);
+        if (threadIdx.x < 12) {
+            F->prog[threadIdx.x] = 0;
+            F->front[threadIdx.x] = (int)threadIdx.x < nsw ? i0 + (int)threadIdx.x : n;
+        }
+        if (threadIdx.x == 0) {
+            F->loaded = i0; F->freed = i0; F->avail = 0;
+            F->wturn = 0; F->wclaim = i0; F->wpub = i0;
+        }
+#ifdef BRD_S2TRACE
+        if (threadIdx.x == 0 && TRB(beta)) {
+            g_s2tr.bundle[beta - kTrB0][0] = __builtin_amdgcn_s_memrealtime();
+            g_s2tr.bundle[beta - kTrB0][2] = blockIdx.x;
+            g_s2tr.bundle[beta - kTrB0][3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+        }
+#endif
+        __syncthreads();
+
+        if (wave < nsw) {
+            // ---------------- compute wave: sweep i0 + wave ----------------
+            const int i = i0 + wave;
+            SweepIter it;
+            it.init(n, n, b, i, sigma);
+            const int prev_ntask = wave > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
+            for (int t = 0; t < it.ntask; ++t) {
+                bool right;
+                const Win w = it.task(t, right);
+                int spins = 0;
+                TRT(beta, wave, t, 0);
+                if (wave > 0) {   // lag 3 against the previous sweep (tests/test_stage2_schedule.py)
+                    const int need = min(t + 4, prev_ntask);
+                    while (lds_ld(&F->prog[wave - 1]) < need) {
+                        __builtin_amdgcn_s_sleep(0);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 12); break; }
+                    }
+                }
+                const int nr = w.i2 - w.i1, nc = w.j2 - w.j1;
+                TRT(beta, wave, t, 1);
+                if (nr > 0 && nc > 0) {
+                    while (lds_ld(&F->loaded) < w.i2) {
+                        __builtin_amdgcn_s_sleep(0);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 13); break; }
+                    }
+                    TRT(beta, wave, t, 2);
+                    asm volatile("" ::: "memory");
+                    if (right) {
+                        if (nr == 2 * b && nc == b) s2_right_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane);
+                        else                        s2_right_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane);
+                    } else {
+                        if (nr == b && nc == 2 * b) s2_left_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane);
+                        else                        s2_left_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane);
+                    }
+                    asm volatile("" ::: "memory");
+                }
+                TRT(beta, wave, t, 3);
+                // LDS executes this wave's operations in order: the window's ring
+                // stores land before these words.
+                if (lane == 0) {
+                    lds_st(&F->front[wave], it.next_top(t));
+                    lds_st(&F->prog[wave], t + 1);
+                }
+            }
+        } else if (wave == S) {
+            // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
+            // (the k_band2bd_bundle loader: one global_load_lds_dwordx4 per
+            // interior row, up to kFly rows in flight, published oldest first in
+            // chunks of kChunk behind counted vmcnt waits; edge rows through
+            // registers)
+            const int row_q = P * (int)sizeof(T) / 16;
+            const unsigned row_bytes = (unsigned)(P * (int)sizeof(T));
+            const unsigned ring_lds = (unsigned)(uintptr_t)ring;
+            const unsigned ring_end = ring_lds + (unsigned)R * row_bytes;
+            const int dma_hi = (int)(((long)(n - 1) * lda + n + (b - 1) - P) / (lda + 1));
+            int ra = i0, rl = i0, spins = 0;
+            unsigned dst = ring_lds + (unsigned)rg.slot(i0) * row_bytes;
+            const char *src = (const char *)(A + (long)i0 * lda + i0 - (b - 1)) + 16 * lane;
+            const long rstep = (lda + 1) * (long)sizeof(T);
+            const bool dma_lane = lane < row_q;
+            while (rl < n) {
+                const int av = lds_ld(&F->avail);
+                const int fr = lds_ld(&F->freed);
+                const int lim = __builtin_amdgcn_readfirstlane(min(min(av, fr + R), min(n, rl + kFly)));
+                bool moved = false;
+                if (ra < lim) {
+                    if (ra >= 1 && ra <= dma_hi) {
+                        const int k = min(lim, dma_hi + 1) - ra;
+                        if (dma_lane) {
+                            const char *p = src;
+                            unsigned d = dst;
+                            for (int q = 0; q < k; ++q) {
+                                dma16_sc1(p, d);
+                                p += rstep;
+                                d += row_bytes;
+                                if (d == ring_end) d = ring_lds;
+                            }
+                        }
+                        src += (long)k * rstep;
+                        dst += (unsigned)k * row_bytes;
+                        if (dst >= ring_end) dst -= ring_end - ring_lds;
+                        ra += k;
+                        moved = true;
+                        TRP(beta, 5, ra);
+                    } else if (ra == rl) {   // edge row, once the DMAs before it have landed
+                        load_edge_row<T>(A, lda, n, b, ra, (T *)((char *)ring + (dst - ring_lds)), row_q, lane);
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        ++ra;
+                        rl = ra;
+                        src += rstep;
+                        dst += row_bytes;
+                        if (dst == ring_end) dst = ring_lds;
+                        if (lane == 0) lds_st(&F->loaded, rl);
+                        moved = true;
+                    }
+                }
+                if (ra > rl) {
+                    const int keep = max(0, ra - rl - kChunk);
+                    wait_vmcnt(keep);
+                    rl = ra - keep;
+                    if (lane == 0) lds_st(&F->loaded, rl);
+                    TRP(beta, 0, rl);
+                    spins = 0;
+                } else if (!moved) {
+                    __builtin_amdgcn_s_sleep(0);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 14); break; }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (wave == S + 1 + kSweepWriters) {
+            // ---------------- poller wave: rows bundle beta-1 has written back ----------------
+            if (beta == 0) {
+                if (lane == 0) lds_st(&F->avail, n);
+            } else {
+                const int *done_prev = rows_done + beta - 1;
+                int av = 0, spins = 0;
+                while (av < n) {
+                    const int v = __builtin_amdgcn_readfirstlane(ld_c(done_prev));
+                    if (v != av) {
+                        av = v;
+                        if (lane == 0) lds_st(&F->avail, v);
+                        TRP(beta, 2, v);
+                        spins = 0;
+                    } else {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 16); break; }
+                    }
+                }
+            }
+        } else if (wave > S && wave <= S + kSweepWriters) {
+            // ---------------- writer waves: ring -> HBM ----------------
+            // Batches of at most kWriteRows rows below all fronts (no sweep of
+            // the bundle touches them again), dealt alternately to the writer
+            // waves so that one batch's drain overlaps the next batch's stores
+            // (a single writer that drains each batch before taking the next
+            // held the whole chain to one batch per drain latency).  Per batch:
+            // claim its rows (in turn), ring -> registers, free the slots (in
+            // row order), 16-byte sc1 stores, drain, publish rows_done[beta]
+            // (in row order).
+            const int wi = wave - S - 1;
+            const int row_q = P * (int)sizeof(T) / 16;
+            const long gstep = (lda + 1) * (long)sizeof(T);
+            for (int q = wi;; q += kSweepWriters) {
+                int spins = 0;
+                while (lds_ld(&F->wturn) != q) {   // the previous batch is claimed
+                    __builtin_amdgcn_s_sleep(0);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
+                }
+                const int wb = __builtin_amdgcn_readfirstlane(lds_ld(&F->wclaim));
+                if (wb >= n) {   // all rows claimed: let the other writer see it too
+                    if (lane == 0) lds_st(&F->wturn, q + 1);
+                    break;
+                }
+                int wt = wb;
+                spins = 0;
+                for (;;) {
+                    int fmin = n;
+                    for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_ld(&F->front[s]));
+                    wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_ld(&F->loaded)), wb + kWriteRows));
+                    if (wt > wb) break;
+                    __builtin_amdgcn_s_sleep(0);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
+                }
+                if (wt <= wb) break;
+                if (lane == 0) {
+                    lds_st(&F->wclaim, wt);
+                    lds_st(&F->wturn, q + 1);
+                }
+                TRP(beta, 3, wb);
+                const int k = wt - wb;
+                const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
+                // ring -> registers -> HBM in two halves of kWriteRows / 2 rows
+                // (registers); the slots are freed (in row order) once all rows
+                // are read
+                constexpr int kH = kWriteRows / 2;
+                const int sl0 = rg.slot(wb);
+                for (int h = 0; h < 2; ++h) {
+                    const int r0 = h * kH;
+                    if (r0 >= k) break;
+                    u32x4 v[kH];
+                    const int sl = sl0 + r0 >= R ? sl0 + r0 - R : sl0 + r0;
+                    const u32x4 *srow = (const u32x4 *)(ring + sl * P) + (lane < row_q ? lane : 0);
+                    const int wrap = R - sl;
+#pragma unroll
+                    for (int rr = 0; rr < kH; ++rr)
+                        if (r0 + rr < k) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (h == 1 || r0 + kH >= k) {
+                        spins = 0;
+                        while (lds_ld(&F->freed) != wb) {   // slots are freed in row order
+                            __builtin_amdgcn_s_sleep(0);
+                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
+                        }
+                        if (lane == 0) lds_st(&F->freed, wt);
+                        TRP(beta, 6, wt);
+                    }
+                    if (interior) {
+                        if (lane < row_q) {
+                            const char *g = (const char *)(A + (long)(wb + r0) * lda + wb + r0 - (b - 1)) + 16 * lane;
+#pragma unroll
+                            for (int rr = 0; rr < kH; ++rr) {
+                                if (r0 + rr < k) st16_sc1((void *)g, v[rr]);
+                                g += gstep;
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int rr = 0; rr < kH; ++rr) {
+                            const int r = wb + r0 + rr;
+                            if (r0 + rr < k && lane < row_q) {
+                                T *ge = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
+                                const int cc0 = r - (b - 1) + lane * kEpp<T>;
+                                T e[kEpp<T>];
+                                __builtin_memcpy(e, &v[rr], 16);
+#pragma unroll
+                                for (int kk = 0; kk < kEpp<T>; ++kk)
+                                    if (cc0 + kk >= 0 && cc0 + kk < n) st_c(ge + kk, e[kk]);
+                            }
+                        }
+                    }
+                }
+                TRP(beta, 4, wt);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                spins = 0;
+                while (lds_ld(&F->wpub) != wb) {   // rows_done advances in row order
+                    __builtin_amdgcn_s_sleep(0);
+                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
+                }
+                if (lane == 0) {
+                    st_c(rows_done + beta, wt);
+                    lds_st(&F->wpub, wt);
+                }
+                TRP(beta, 1, wt);
+            }
+        }
+        __syncthreads();
+#ifdef BRD_S2TRACE
+        if (threadIdx.x == 0 && TRB(beta)) g_s2tr.bundle[beta - kTrB0][1] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
+}
+
+#ifdef BRD_S2TRACE
+extern "C" int brd_dbg_s2trace(void *dst, size_t bytes, int reset) {
+    if (reset) {
+        static S2Trace z;
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s2tr), &z, sizeof(S2Trace));
+    }
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_s2tr), bytes < sizeof(S2Trace) ? bytes : sizeof(S2Trace));
+}
+#endif
+
 template <typename T>
 __global__ void k_extract(const T *A, int n, long lda, T *d, T *e)
 {
@@ -1239,6 +1599,34 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
     return false;
 }
 
+// k_sweeps geometry: S sweeps per bundle (one compute wave each) and a ring of
+// R rows.  The most sweeps whose ring keeps kSweepSlack rows beyond
+// ring_min_rows (the loader's run-ahead: one 32-row release of the trailing
+// sweep in flight), then the largest ring that fits.  BRD_S2_SWEEPS caps S
+// (tuning).
+constexpr int kSweepSlack = 40;
+template <typename T>
+static size_t sweeps_lds_bytes(int R) {
+    return (((size_t)R * ring_pitch<T>(32) * sizeof(T) + 15) & ~(size_t)15) + sizeof(SweepFlags);
+}
+template <typename T>
+static bool sweeps_plan(int n, int &S, int &R) {
+    const size_t budget = 160 * 1024;
+    static const char *senv = getenv("BRD_S2_SWEEPS");
+    int smax = sweeps_max_threads<T>() / 64 - 2 - kSweepWriters;
+    if (smax > 12) smax = 12;
+    if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
+    for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
+        const int rmin = ring_min_rows(32, S) + kSweepSlack;
+        if (sweeps_lds_bytes<T>(rmin) <= budget) {
+            R = rmin;
+            while (R < n + 1 && sweeps_lds_bytes<T>(R + 1) <= budget) ++R;
+            return true;
+        }
+    }
+    return false;
+}
+
 // Workgroups of `fn` (block threads, dynamic LDS bytes) that can be resident
 // at once on the device: the persistent sweep kernels hand bundles / sweeps
 // round-robin and wait on their predecessors, so every workgroup of the grid
@@ -1264,6 +1652,21 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
     const bool pipe = sel && sel[0] == 'p';
     int S = 0, R = 0;
     const bool fast32 = !exact_order && b == 32;
+    const char *legacy = getenv("BRD_S2_LEGACY");   // 1: k_band2bd_bundle for b = 32 fast too (A/B)
+    if (!pipe && fast32 && !(legacy && legacy[0] == '1') && n >= 64 && sweeps_plan<T>(n, S, R)) {
+        const int nbundles = (n - 1 + S - 1) / S;
+        const dim3 block(64 * (S + 2 + kSweepWriters));
+        const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
+        const void *fn = (const void *)k_sweeps<T>;
+        const size_t lds = sweeps_lds_bytes<T>(R);
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        const int cap = coresident_limit(fn, (int)block.x, lds);
+        if (cap < 1) return hipErrorInvalidConfiguration;
+        const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
+        hipLaunchKernelGGL((k_sweeps<T>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
+        return hipGetLastError();
+    }
     const int W = fast32 ? s2_waves_per_sweep() : 1;
     const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, S, R)
                     : W == 4    ? bundle_plan<T, false, 4>(n, b, S, R)

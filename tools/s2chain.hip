@@ -1,0 +1,148 @@
+// Stage-2 window-chain micro-benchmark (developer tool, not product).
+//
+// One workgroup runs S sweeps of interior windows on an LDS ring of band rows
+// with the lag-3 rule between consecutive sweeps (LDS progress words), no IO
+// waves: the pace of an unconstrained bundle.  Prints cycles (s_memtime) per
+// window step for each sweep.
+//   mode 0: production windows split over a wave pair (win_*_multi, W = 2)
+//   mode 1: production single-wave full windows (win_*_full, W = 1)
+//   mode 2: the new single-wave windows (brd_s2win.h)
+//   mode 3: the new wave-pair windows (brd_s2win.h, W = 2)
+#include "../svdsolver_amd/csrc/brd_stage2.hip"
+#include "../svdsolver_amd/csrc/brd_s2win.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+namespace brd {
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain(int S, int R, int npairs, int noise, unsigned long long *out) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr int B = 32;
+    const int P = ring_pitch<T>(B);
+    T *ring = (T *)smem;
+    int *prog = (int *)(smem + (size_t)R * P * sizeof(T));   // 16 words
+    int *xr = prog + 16;                                      // 16 words
+    constexpr int W = (MODE == 0 || MODE == 3) ? 2 : 1;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
+    const RingAcc<T> acc{ring, P, R, B - 1, magic};
+    for (int e = threadIdx.x; e < R * P; e += blockDim.x) {
+        unsigned h = (unsigned)e * 2654435761u;
+        ring[e] = (T)(1.0 + (double)(h >> 8) / 16777216.0);
+    }
+    if (threadIdx.x < 32) prog[threadIdx.x] = 0;
+    __syncthreads();
+    if (wave >= W * S) {
+        // background LDS traffic: read + write 768-B rows (a loader / writer stand-in)
+        if (noise) {
+            u32x4 *rp = (u32x4 *)ring;
+            const int rq = P * (int)sizeof(T) / 16;
+            for (int k = 0; k < npairs * 32; ++k) {
+                const int r = (k * 7) % R;
+                if (lane < rq) {
+                    u32x4 v = rp[r * rq + lane];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    rp[r * rq + lane] = v;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        return;
+    }
+    const int sw = wave / W, pw = wave - sw * W;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const int ntask = 2 * npairs;
+    for (int t = 0; t < ntask; ++t) {
+        if (sw > 0) {
+            const int need = min(t + 4, ntask);
+            for (int spin = 0; spin < (1 << 22); ++spin) {
+                int m = __hip_atomic_load(prog + W * (sw - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (W == 2) m = min(m, __hip_atomic_load(prog + W * (sw - 1) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (m >= need) break;
+                __builtin_amdgcn_s_sleep(0);
+            }
+        }
+        if (W == 2) {
+            for (int spin = 0; spin < (1 << 22); ++spin) {
+                const int m = min(__hip_atomic_load(prog + W * sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                                  __hip_atomic_load(prog + W * sw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (m >= t) break;
+                __builtin_amdgcn_s_sleep(0);
+            }
+        }
+        asm volatile("" ::: "memory");
+        const int p = t >> 1;
+        const bool right = (t & 1) == 0;
+        const int i1 = sw + 1 + 32 * (p + 1) + (right ? 0 : 32);   // virtual rows (ring slot = row mod R)
+        if constexpr (MODE == 0) {
+            const MultiSync ms{xr + W * sw, pw, W, t + 1};
+            const int L = 64 * pw + lane;
+            if (right) win_right_multi<T, B, 2, true>(acc, i1, i1 + 64, i1 + 32, i1 + 64, L, lane, ms);
+            else       win_left_multi<T, B, 2, true>(acc, i1, i1 + 32, i1, i1 + 64, L, lane, ms);
+        } else if constexpr (MODE == 1) {
+            if (right) win_right_full<T, B>(acc, i1, i1 + 32, lane);
+            else       win_left_full<T, B>(acc, i1, i1, lane);
+        } else if constexpr (MODE == 2) {
+            const S2Ring<T> rg{ring, P, R, magic};
+            if (right) s2_right_w1<T, true>(rg, i1, i1 + 32, 64, 32, lane);
+            else       s2_left_w1<T, true>(rg, i1, i1, 32, 64, lane);
+        } else {
+            const S2Ring<T> rg{ring, P, R, magic};
+            S2Pair pr{xr + W * sw, pw, t + 1};
+            if (right) s2_right_w2<T, true>(rg, i1, 64, 32, lane, pr);
+            else       s2_left_w2<T, true>(rg, i1, 32, 64, lane, pr);
+        }
+        asm volatile("" ::: "memory");
+        if (lane == 0) __hip_atomic_store(prog + wave, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[wave] = t1 - t0;
+    // keep the ring live (the compiler must not drop the windows' stores)
+    if (threadIdx.x == 0) out[63] = (unsigned long long)(ring[7] != ring[7]);
+}
+
+}  // namespace brd
+
+template <typename T, int MODE>
+static void run(int S, int npairs, int noise) {
+    const int P = brd::ring_pitch<T>(32);
+    int R = (160 * 1024 - 256) / (P * (int)sizeof(T));
+    if (R > 400) R = 400;
+    const size_t lds = (size_t)R * P * sizeof(T) + 256;
+    constexpr int W = (MODE == 0 || MODE == 3) ? 2 : 1;
+    unsigned long long *o;
+    (void)hipMalloc(&o, 64 * 8);
+    (void)hipMemset(o, 0, 64 * 8);
+    auto fn = brd::k_chain<T, MODE>;
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int threads = 64 * (W * S + (noise ? 2 : 0));
+    hipLaunchKernelGGL(fn, dim3(1), dim3(threads), lds, 0, S, R, npairs, noise, o);
+    unsigned long long h[64];
+    (void)hipMemcpy(h, o, sizeof(h), hipMemcpyDeviceToHost);
+    const hipError_t e = hipGetLastError();
+    printf("%s mode %d S=%d W=%d noise=%d R=%d: %s cycles/window:", sizeof(T) == 8 ? "f64" : "f32", MODE, S, W,
+           noise, R, hipGetErrorString(e));
+    for (int w = 0; w < W * S; w += W) printf(" %.0f", (double)h[w] / (2.0 * npairs));
+    printf("\n");
+    (void)hipFree(o);
+}
+
+int main(int argc, char **argv) {
+    const int npairs = argc > 1 ? atoi(argv[1]) : 400;
+    for (int noise = 0; noise <= 1; ++noise)
+        for (int S = 1; S <= 3; ++S) {
+            run<double, 0>(S, npairs, noise);
+            run<double, 1>(S, npairs, noise);
+            run<double, 2>(S, npairs, noise);
+            run<double, 3>(S, npairs, noise);
+        }
+    for (int S = 1; S <= 5; S += 2) {
+        run<float, 0>(S, npairs, 0);
+        run<float, 2>(S, npairs, 0);
+        run<float, 3>(S, npairs, 0);
+    }
+    return 0;
+}

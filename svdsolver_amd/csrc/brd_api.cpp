@@ -263,7 +263,7 @@ static void trim_stage(Ctx::Slot &w) {
     }
 }
 
-static int device_cus() {
+int api_device_cus() {
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -281,7 +281,7 @@ int api_apply_target() {
     const int ov = g_ctx.overlap_cus;
     static const char *tenv = getenv("BRD_S1_TARGET");   // tuning: workgroups per apply launch
     if (tenv && atoi(tenv) > 0) return atoi(tenv);
-    return ov > 0 ? std::max(32, device_cus() - ov) : device_cus();
+    return ov > 0 ? std::max(32, api_device_cus() - ov) : api_device_cus();
 }
 
 // Least slabs per apply workgroup at tree level `level`.  Beside other work
@@ -306,7 +306,7 @@ static int s2_waves() {
     if (g_ctx.overlap_cus > 0) return g_ctx.overlap_cus;
     static int nw = 0;
     if (!nw) {
-        nw = device_cus();   // launch_band2bd clamps to the co-resident capacity
+        nw = api_device_cus();   // launch_band2bd clamps to the co-resident capacity
         // Bundles that can make progress at once are bounded by the chain
         // (~one bundle lifetime / one hand-off, < 64 at N <= 16384): a smaller
         // grid leaves CUs free for work on another stream (tuning override).
@@ -710,7 +710,7 @@ int brd_set_stream(void *hip_stream) {
 
 int brd_set_overlap(int s2_cus) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
-    const int cus = brd::device_cus();
+    const int cus = brd::api_device_cus();
     if (s2_cus < 0 || s2_cus >= cus)
         return brd::fail(BRD_EINVAL, "brd_set_overlap: s2_cus=%d outside [0,%d) (device CUs)", s2_cus, cus);
     brd::g_ctx.overlap_cus = s2_cus;

@@ -128,6 +128,10 @@ constexpr int kCW = 128;  // most workgroups per panel (M <= kCW kCT rows; the d
                           // is padded per rank: P x roundup(local columns, 256) rows)
 constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace ([32][kQS]: a lane per row, coalesced)
 
+#ifndef BRD_HANDOFF_RELAXED
+#define BRD_HANDOFF_RELAXED 0   // 1: the relaxed (guide-measured) form of the prep / read-pass hand-offs (A/B)
+#endif
+constexpr int kBlkMaxRanks = 16;   // the blocked distributed path's most ranks (gathered row panel blocks)
 struct CqrArgs {
     const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
     int M;
@@ -143,6 +147,8 @@ struct CqrArgs {
     long blk, bstride;                // blk > 0: the source is stored in blocks of blk rows (a multiple of
                                       // kCT), block q at src + q bstride, row i of it at (i mod blk) si
                                       // (the distributed path's gathered [rank][32][slot] row panel)
+    int nreal[kBlkMaxRanks];          // blk > 0: real (not zero-padded) rows of block q; rows
+                                      // i mod blk >= nreal[i / blk] are padding and stay zero in Q
 };
 
 // scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the

@@ -419,7 +419,15 @@ __device__ __attribute__((noinline)) bool chol_def(const double (&G)[32][kSP], d
     return chol_wave<true>(G, R, Rw, lane, mask);
 }
 
-__device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, int M, int nwg, double (&x)[32]) {
+// a zero-padded row of the distributed path's gathered row panel (CqrArgs::nreal)
+__device__ __forceinline__ bool cqr_pad_row(const CqrArgs &a, int i) {
+    if (a.blk <= 0) return false;
+    const int q = (int)(i / a.blk);
+    return q < kBlkMaxRanks && (int)(i - q * a.blk) >= a.nreal[q];
+}
+
+__device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, const CqrArgs &a, int nwg, double (&x)[32]) {
+    const int M = a.M;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     __shared__ unsigned dmask;
     gram_sum_all(L, W.gp2, L.scl, nwg);
@@ -441,9 +449,13 @@ __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, int 
 #pragma unroll
         for (int t = 0; t < 32; ++t) y[t] = W.q1[t * kQS + i];
         if (mask) {   // (chol_wave<true> made the solve leave these columns alone)
+            // padding rows keep their zero: a completion there would give Q
+            // rows the caller drops (k_dist_scatter_u), and the kept rows of Q
+            // would not be orthonormal
+            const bool pad = cqr_pad_row(a, i);
 #pragma unroll
             for (int t = 0; t < 32; ++t)
-                if (mask >> t & 1u) y[t] = cqr_completion(i, t, cscale);
+                if (mask >> t & 1u) y[t] = pad ? 0.0 : cqr_completion(i, t, cscale);
         }
         trsm_row(y, L.r2w);
         if (i >= M) {
@@ -524,7 +536,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         for (int t = 0; t < 32; ++t) x[t] = W.q1[t * kQS + i];
     }
     if (!zero) {
-        if (sh) cqr_shifted_pass(L, W, a.M, nwg, x);
+        if (sh) cqr_shifted_pass(L, W, a, nwg, x);
         else    gram_sum_all(L, W.gp2, L.scl, nwg);
         __syncthreads();
         // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the

@@ -112,13 +112,22 @@ __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, in
     const int per = 256 / ipw, grp = wg / per, b0 = grp * per;
     const int members = min(per, (a.items - grp * 256 + ipw - 1) / ipw);
     if (tl == 0) {
-#ifdef BRD_GRAM_ACQREL
-        const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-#else
+        // the arrival publishes this workgroup's record (release) and the last
+        // arriver acquires the others' (the memory model's form of
+        // the guide's measured sc1 hand-off; BRD_HANDOFF_RELAXED=1 builds the
+        // relaxed form for A/B)
+#if BRD_HANDOFF_RELAXED
         const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        const int old = __hip_atomic_fetch_add(a.gcnt + grp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #endif
         const int last = old == members - 1;
-        if (last) __hip_atomic_store(a.gcnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) {
+#if !BRD_HANDOFF_RELAXED
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+            __hip_atomic_store(a.gcnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         *sflag = last;
     }
     __syncthreads();

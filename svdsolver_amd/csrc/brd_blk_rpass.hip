@@ -413,10 +413,19 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
             const int cnt0 = (a.ns - 1) / a.wst + 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) {
+            if (tid == 0) {   // release / acquire as in brd_blk_prep.hip's Gram fold
+#if BRD_HANDOFF_RELAXED
                 const int old = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+                const int old = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                 const int last = old == cnt0 - 1;
-                if (last) __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (last) {
+#if !BRD_HANDOFF_RELAXED
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+                    __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 vlast = last;
             }
             __syncthreads();

@@ -277,10 +277,11 @@ int dtype_of() { return sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32; }
 // as on one GPU), unless BRD_S1_BLOCKED=0; BRD_DIST_BLOCKED=0 keeps the
 // per-panel loop throughout (A/B).
 template <typename T>
-int dist_blocked_columns(int m, int n, int lda, int b, const T *A) {
+int dist_blocked_columns(int m, int n, int lda, int b, int P, const T *A) {
     const char *e1 = getenv("BRD_S1_BLOCKED"), *e2 = getenv("BRD_DIST_BLOCKED");
     if ((e1 && e1[0] == '0') || (e2 && e2[0] == '0')) return 0;
     if (sizeof(T) != 8 || b != 32 || lda % 2 != 0 || ((uintptr_t)A % 16) != 0) return 0;
+    if (!blk_dist_fits(n, P)) return 0;   // the per-panel loop throughout
     return blk_columns(m, n, b);
 }
 
@@ -291,14 +292,14 @@ int ge2band_dist(T *A, int m, int n, int lda, int b, hipStream_t s) {
     const int P = C.nranks, me = C.rank;
     const int n_loc = local_cols(n, b, P, me);
     if (lda < std::max(n_loc, 1)) return api_fail(BRD_EINVAL, "lda_loc smaller than the local column count");
-    const int kend = dist_blocked_columns<T>(m, n, lda, b, A);
+    if (P * b > kRmax) return api_fail(BRD_EUNSUPPORTED, "nranks * b must be <= 512 (one-level tree root)");
+    const int kend = dist_blocked_columns<T>(m, n, lda, b, P, A);
     if (kend > 0) {
         int *err = api_s1_err();
         if (!err) return api_fail(BRD_ENOMEM, "stage-1 error word allocation failed");
         D_TRY(g_dws.ensure(blk_dist_ws_bytes(m, n, P, me, sizeof(T)), s));
         D_TRY(blk_ge2band_dist<T>(A, m, n, lda, C, g_dws.mem, s, api_apply_target(), err));
     }
-    if (P * b > kRmax) return api_fail(BRD_EUNSUPPORTED, "nranks * b must be <= 512 (one-level tree root)");
     const size_t sz = sizeof(T);
     // workspace: QR / local-LQ tree, root tree, panel, local R, gathered R, stack, W
     const size_t ws_tree = std::max(tree_ws_bytes(make_tree(m, b), sz),

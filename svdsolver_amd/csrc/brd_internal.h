@@ -97,6 +97,10 @@ inline int dist_local_cols(int n, int b, int P, int r) {
 // shard.  ws: blk_dist_ws_bytes.  The caller finishes the remaining panels
 // with the per-panel distributed loop.
 size_t blk_dist_ws_bytes(int m, int n, int P, int rank, size_t elem);
+// whether the blocked distributed form can run at all: its gathered row panel
+// (P slots of dist_slot_rows rows) fits one panel QR (kCW kCT rows) and P fits
+// the panel QR's per-block row counts
+bool blk_dist_fits(int n, int P);
 template <typename T>
 int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *ws, hipStream_t s, int target, int *err);
 
@@ -116,6 +120,7 @@ hipError_t launch_bdsvd_dev(const T *d, const T *e, int n, T *sv, T *ws, hipStre
 int api_fail(int code, const char *msg);           // sets brd_last_error, returns code
 hipStream_t api_stream();                          // the library stream
 int api_apply_target();                            // workgroups per stage-1 apply launch
+int api_device_cus();                              // CUs of the current device (whatever brd_set_overlap reserves)
 int api_min_run(int level);                        // least slabs per apply workgroup at a tree level
 bool api_overlap_active();                         // brd_set_overlap reservation in force
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);

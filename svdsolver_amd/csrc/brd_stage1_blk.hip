@@ -91,6 +91,9 @@ int blk_columns(int m, int n, int b) {
 // stream, but the two forms round the K1 sums differently, and a matrix's
 // band would then depend on whether it ran in a stream: not kept.
 // BRD_PREP_SPLIT=0 / 1 forces either form for A/B runs.)
+// cus: the device's CUs, not the overlap-reduced apply target, so that the
+// split (and with it the rounding of the K1 sums) is the same whether or not
+// the call runs beside stage 2
 static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
@@ -171,8 +174,9 @@ template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
                              hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr,
-                             long blk = 0, long bstride = 0, bool gram_done = false) {
+                             long blk = 0, long bstride = 0, bool gram_done = false, const int *nreal = nullptr) {
     CqrArgs a;
+    for (int q = 0; q < kBlkMaxRanks; ++q) a.nreal[q] = nreal ? nreal[q] : 0;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
     a.vdst2 = vdst2; a.vsi2 = vsi2; a.vst2 = vst2;
@@ -256,7 +260,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c; p.zfill = 0;
                 p.upatch = x_patch ? 1 : 0;
                 gram_into(p, fold_qr);
-                launch_k_prep<T>(false, prep_grid(p, target), p, s);
+                launch_k_prep<T>(false, prep_grid(p, api_device_cus()), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -281,7 +285,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c + 32; p.zfill = 0;
                 p.vpatch = yfold ? 1 : 0;
                 gram_into(p, fold_lq);
-                launch_k_prep<T>(true, prep_grid(p, target), p, s);
+                launch_k_prep<T>(true, prep_grid(p, api_device_cus()), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -313,7 +317,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
             p.cc = k1; p.zfill = 0;
-            launch_k_prep<T>(false, prep_grid(p, target), p, s);
+            launch_k_prep<T>(false, prep_grid(p, api_device_cus()), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -399,6 +403,9 @@ DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
 }  // namespace
 
 size_t blk_dist_ws_bytes(int m, int n, int P, int rank, size_t elem) { return dist_blk_layout(m, n, P, rank, elem).total; }
+bool blk_dist_fits(int n, int P) {
+    return P >= 1 && P <= kBlkMaxRanks && (long)P * dist_slot_rows(n, P, 0) <= (long)kCW * kCT;
+}
 
 #define BD_HIP(expr)                                                                          \
     do {                                                                                      \
@@ -459,7 +466,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             if (j > 0) {
                 PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1),
                                    sg0, lco);
-                launch_k_prep<T>(false, prep_grid(pa, target), pa, s);
+                launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
             const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
@@ -483,7 +490,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
                 pa.Qp = slot; pa.mq = cnt; pa.zfill = (int)cnt;   // [32][cnt]: coalesced, as on one GPU
-                launch_k_prep<T>(true, prep_grid(pa, target), pa, s);
+                launch_k_prep<T>(true, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
             if (P > 1) BD_TRY(C.allgather(slot, gat, (size_t)cnt * 32 * sizeof(T), s));
@@ -492,9 +499,14 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                                       hipMemcpyDeviceToDevice, s));
             const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
                              own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
+            int nreal[kBlkMaxRanks] = {};   // block q of the rotated panel: rank (o2 + q) mod P's trailing columns
+            for (int q = 0; q < P && q < kBlkMaxRanks; ++q) {
+                const int r = (o2 + q) % P;
+                nreal[q] = std::max(0, dist_local_cols(n, 32, P, r) - dist_panels_before(p + 1, P, r) * 32);
+            }
             BD_HIP(launch_cqr<T>(gat + (size_t)o2 * cnt * 32, 1, cnt, (int)(P * cnt), Vg, 32, 1, nullptr, 0, 0, Sj,
                                  own2 ? A + (size_t)c * lda + lcs : nullptr, 1, lda, ws, Ly, err, s, true, fl, 0,
-                                 nullptr, cnt, cnt * 32));
+                                 nullptr, cnt, cnt * 32, false, nreal));
             launch_dist_scatter_u<T>(Vg, (long)((me - o2 + P) % P) * cnt, nc, RwT, ldr, 128 + 32 * j, lcs, Ub, A, lda,
                                      c, own2 ? 32 : 0, s);
             // ---- X pass (local columns), partials summed and all-reduced ------------
@@ -513,7 +525,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         const int k1 = k0 + NBMAX * 32;
         {
             PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
-            launch_k_prep<T>(false, prep_grid(pa, target), pa, s);
+            launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
             BD_HIP(hipGetLastError());
         }
         const long lck = (long)dist_panels_before(k1 / 32, P, me) * 32;

@@ -1218,6 +1218,7 @@ struct S2Trace {
     unsigned long long pub[kTrNB][8][kTrPub][2];       // loader / writer / poller / claim / issued / ldissue / freed
     int npub[kTrNB][8];
     unsigned long long bundle[kTrNB][4];               // start, end, block, xcc
+    unsigned long long wr[kTrNB][256][8];             // writer batch q: stamps
 };
 __device__ S2Trace g_s2tr;
 #define TRB(beta) ((beta) >= kTrB0 && (beta) < kTrB0 + kTrNB)
@@ -1236,9 +1237,15 @@ __device__ S2Trace g_s2tr;
             }                                                                                   \
         }                                                                                       \
     } while (0)
+#define TRW(beta, q, k)                                                                         \
+    do {                                                                                        \
+        if (TRB(beta) && (q) < 256 && lane == 0)                                                \
+            g_s2tr.wr[(beta) - kTrB0][q][k] = __builtin_amdgcn_s_memrealtime();                 \
+    } while (0)
 #else
 #define TRT(beta, w, t, k) do {} while (0)
 #define TRP(beta, kind, val) do {} while (0)
+#define TRW(beta, q, k) do {} while (0)
 #endif
 
 template <typename T> constexpr int sweeps_max_threads() { return sizeof(T) == 8 ? 512 : 768; }
@@ -1368,6 +1375,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                         ra += k;
                         moved = true;
                         TRP(beta, 5, ra);
+                        TRP(beta, 7, (av <= fr + R ? 0 : 1) + (lim == rl + kFly ? 2 : 0));
                     } else if (ra == rl) {   // edge row, once the DMAs before it have landed
                         load_edge_row<T>(A, lda, n, b, ra, (T *)((char *)ring + (dst - ring_lds)), row_q, lane);
                         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1453,6 +1461,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                     lds_st(&F->wturn, q + 1);
                 }
                 TRP(beta, 3, wb);
+                TRW(beta, q, 0);
                 const int k = wt - wb;
                 const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
                 // ring -> registers -> HBM in two halves of kWriteRows / 2 rows
@@ -1471,15 +1480,18 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                     for (int rr = 0; rr < kH; ++rr)
                         if (r0 + rr < k) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    if (h == 1 || r0 + kH >= k) {
+                    TRW(beta, q, 1 + 3 * h);
+                    {   // these rows' slots are free (freed advances in row order)
+                        const int fr = min(wt, wb + r0 + kH);
                         spins = 0;
-                        while (lds_ld(&F->freed) != wb) {   // slots are freed in row order
+                        while (lds_ld(&F->freed) != wb + r0) {
                             __builtin_amdgcn_s_sleep(0);
                             if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
                         }
-                        if (lane == 0) lds_st(&F->freed, wt);
-                        TRP(beta, 6, wt);
+                        if (lane == 0) lds_st(&F->freed, fr);
+                        TRP(beta, 6, fr);
                     }
+                    TRW(beta, q, 2 + 3 * h);
                     if (interior) {
                         if (lane < row_q) {
                             const char *g = (const char *)(A + (long)(wb + r0) * lda + wb + r0 - (b - 1)) + 16 * lane;
@@ -1504,9 +1516,11 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                             }
                         }
                     }
+                    TRW(beta, q, 3 + 3 * h);
                 }
                 TRP(beta, 4, wt);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                TRW(beta, q, 7);
                 spins = 0;
                 while (lds_ld(&F->wpub) != wb) {   // rows_done advances in row order
                     __builtin_amdgcn_s_sleep(0);

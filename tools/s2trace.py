@@ -54,7 +54,7 @@ sz_task = NB * 12 * NT * 4 * 8
 sz_pub = NB * 8 * NP * 2 * 8
 sz_npub = NB * 8 * 4
 sz = sz_task + sz_pub + sz_npub + 4 + NB * 4 * 8   # (padding before the 8-byte array)
-buf = (ctypes.c_ubyte * (sz + 64))()
+buf = (ctypes.c_ubyte * (sz + 64 + NB * 256 * 8 * 8))()
 
 g = torch.Generator(device="cuda").manual_seed(n)
 A = torch.rand(n, n, dtype=dt, device="cuda", generator=g) * 5
@@ -65,7 +65,7 @@ for rep in range(2):
     torch.cuda.synchronize()
     d, e = S.band2bd(W, b)
     torch.cuda.synchronize()
-assert fn(buf, sz + 64, 0) == 0
+assert fn(buf, sz + 64 + NB * 256 * 8 * 8, 0) == 0
 raw = bytes(buf)
 task = np.frombuffer(raw, dtype=np.uint64, count=NB * 12 * NT * 4).reshape(NB, 12, NT, 4).astype(np.int64)
 off = sz_task
@@ -75,6 +75,7 @@ npub = np.frombuffer(raw, dtype=np.int32, count=NB * 8, offset=off).reshape(NB, 
 off += sz_npub
 off = (off + 7) // 8 * 8
 bund = np.frombuffer(raw, dtype=np.uint64, count=NB * 4, offset=off).reshape(NB, 4).astype(np.int64)
+wrs = np.frombuffer(raw, dtype=np.uint64, count=NB * 256 * 8, offset=off + NB * 4 * 8).reshape(NB, 256, 8).astype(np.int64)
 
 S_ = None
 for k in range(12):
@@ -189,3 +190,15 @@ for q in range(len(li)):
         lat.append((lo[idx[0], 0] - li[q, 0]) * us)
 print(f"loader: issue -> loaded (median over {len(lat)} issues) {np.median(lat):.2f} us; issues per bundle {len(li)}")
 # what limited each loader issue: avail or freed + R
+
+W_ = wrs[1]
+ok = [q for q in range(256) if W_[q, 0] and W_[q, 7] and W_[q, 6]]
+if ok:
+    d = np.array([[W_[q, j + 1] - W_[q, j] for j in range(7)] for q in ok]) * us
+    print("writer batch phases (median us): claim->rd0 %.2f, ->free0 %.2f, ->st0 %.2f, ->rd1 %.2f, ->free1 %.2f, ->st1 %.2f, ->drained %.2f"
+          % tuple(np.median(d, axis=0)))
+
+lim = series(7)
+if len(lim):
+    v = lim[:, 1]
+    print(f"loader issue limited by: avail {np.mean(v % 2 == 0):.2f}, ring {np.mean(v % 2 == 1):.2f}, in-flight cap {np.mean(v >= 2):.2f}")

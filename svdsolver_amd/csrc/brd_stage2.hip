@@ -1463,60 +1463,70 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 TRP(beta, 3, wb);
                 TRW(beta, q, 0);
                 const int k = wt - wb;
-                const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
-                // ring -> registers -> HBM in two halves of kWriteRows / 2 rows
-                // (registers); the slots are freed (in row order) once all rows
-                // are read
+                // ring -> registers -> HBM in halves of kH rows (registers); each
+                // half's slots are freed (in row order) once it is read.  A full
+                // interior half that does not wrap the ring is straight-line code
+                // (immediate LDS offsets, buffer stores with the row offset in
+                // soffset); anything else goes row by row.
                 constexpr int kH = kWriteRows / 2;
                 const int sl0 = rg.slot(wb);
-                for (int h = 0; h < 2; ++h) {
-                    const int r0 = h * kH;
-                    if (r0 >= k) break;
-                    u32x4 v[kH];
+                const unsigned rstride = (unsigned)gstep;
+                for (int r0 = 0; r0 < k; r0 += kH) {
+                    const int kh = min(kH, k - r0);
                     const int sl = sl0 + r0 >= R ? sl0 + r0 - R : sl0 + r0;
-                    const u32x4 *srow = (const u32x4 *)(ring + sl * P) + (lane < row_q ? lane : 0);
-                    const int wrap = R - sl;
+                    const int rb = wb + r0;
+                    const bool fast = kh == kH && sl + kH <= R && rb >= b - 1 && rb + kH - 1 - (b - 1) + P <= n;
+                    if (fast) {
+                        u32x4 v[kH];
+                        const u32x4 *srow = (const u32x4 *)(ring + sl * P) + (lane < row_q ? lane : 0);
 #pragma unroll
-                    for (int rr = 0; rr < kH; ++rr)
-                        if (r0 + rr < k) v[rr] = srow[(rr < wrap ? rr : rr - R) * (P / kEpp<T>)];
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    TRW(beta, q, 1 + 3 * h);
-                    {   // these rows' slots are free (freed advances in row order)
-                        const int fr = min(wt, wb + r0 + kH);
+                        for (int rr = 0; rr < kH; ++rr) v[rr] = srow[rr * (P / kEpp<T>)];
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        TRW(beta, q, 1 + 3 * (r0 / kH));
                         spins = 0;
-                        while (lds_ld(&F->freed) != wb + r0) {
+                        while (lds_ld(&F->freed) != rb) {   // slots are freed in row order
                             __builtin_amdgcn_s_sleep(0);
                             if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
                         }
-                        if (lane == 0) lds_st(&F->freed, fr);
-                        TRP(beta, 6, fr);
-                    }
-                    TRW(beta, q, 2 + 3 * h);
-                    if (interior) {
+                        if (lane == 0) lds_st(&F->freed, rb + kH);
+                        TRP(beta, 6, rb + kH);
+                        TRW(beta, q, 2 + 3 * (r0 / kH));
                         if (lane < row_q) {
-                            const char *g = (const char *)(A + (long)(wb + r0) * lda + wb + r0 - (b - 1)) + 16 * lane;
+                            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                                (void *)(A + (long)rb * lda + rb - (b - 1)), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-                            for (int rr = 0; rr < kH; ++rr) {
-                                if (r0 + rr < k) st16_sc1((void *)g, v[rr]);
-                                g += gstep;
-                            }
+                            for (int rr = 0; rr < kH; ++rr)
+                                __builtin_amdgcn_raw_buffer_store_b128(v[rr], rs, 16 * lane, rr * rstride, 16);   // sc1
                         }
+                        TRW(beta, q, 3 + 3 * (r0 / kH));
                     } else {
+                        for (int rr = 0; rr < kh; ++rr) {
+                            const int r = rb + rr;
+                            const int sk = sl + rr >= R ? sl + rr - R : sl + rr;
+                            const u32x4 vr = ((const u32x4 *)(ring + sk * P))[lane < row_q ? lane : 0];
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            if (lane < row_q) {
+                                if (r >= b - 1 && r - (b - 1) + P <= n) {
+                                    st16_sc1((void *)((const char *)(A + (long)r * lda + r - (b - 1)) + 16 * lane), vr);
+                                } else {
+                                    T *ge = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
+                                    const int cc0 = r - (b - 1) + lane * kEpp<T>;
+                                    T e[kEpp<T>];
+                                    __builtin_memcpy(e, &vr, 16);
 #pragma unroll
-                        for (int rr = 0; rr < kH; ++rr) {
-                            const int r = wb + r0 + rr;
-                            if (r0 + rr < k && lane < row_q) {
-                                T *ge = A + (long)r * lda + r - (b - 1) + lane * kEpp<T>;
-                                const int cc0 = r - (b - 1) + lane * kEpp<T>;
-                                T e[kEpp<T>];
-                                __builtin_memcpy(e, &v[rr], 16);
-#pragma unroll
-                                for (int kk = 0; kk < kEpp<T>; ++kk)
-                                    if (cc0 + kk >= 0 && cc0 + kk < n) st_c(ge + kk, e[kk]);
+                                    for (int kk = 0; kk < kEpp<T>; ++kk)
+                                        if (cc0 + kk >= 0 && cc0 + kk < n) st_c(ge + kk, e[kk]);
+                                }
                             }
                         }
+                        spins = 0;
+                        while (lds_ld(&F->freed) != rb) {
+                            __builtin_amdgcn_s_sleep(0);
+                            if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
+                        }
+                        if (lane == 0) lds_st(&F->freed, rb + kh);
+                        TRP(beta, 6, rb + kh);
                     }
-                    TRW(beta, q, 3 + 3 * h);
                 }
                 TRP(beta, 4, wt);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     p.add_argument("--band", type=int, default=32)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-n", type=str, default="320,640,1024",
+    p.add_argument("--cpu-n", type=str, default="320,640,1024,2048",
                    help="CPU-baseline sample sizes (comma separated; the largest is the reported sample)")
     p.add_argument("--s2", choices=["compat", "sigma"], default="compat",
                    help="stage-2 geometry: the reference's windows (the headline config) or the "
@@ -181,18 +181,23 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
     coef = np.linalg.lstsq(M, np.ones(len(pts)), rcond=None)[0] if len(pts) >= 2 else np.array([dt / n_s ** 3, 0.0])
     c, d = max(float(coef[0]), 0.0), max(float(coef[1]), 0.0)
     t_ext = c * float(gpu_n) ** 3 + d * float(gpu_n) ** 2
+    phys = hc.get("physical_cores")
+    cores_note = (f"{used} OpenMP threads = the job's CPU share on this host (OMP_NUM_THREADS; the pool sizes "
+                  f"a one-GPU job at 16 CPUs); the host has {phys} physical cores"
+                  + (f": at ideal linear scaling over all of them the reference would reach "
+                     f"{8.0 / 3.0 * n_s ** 3 / dt / 1e9 * phys / max(used, 1):.2f} GFLOP/s at n = {n_s} "
+                     f"(an upper bound, not measured)" if phys and phys > used else ""))
     return {"value": round(8.0 / 3.0 * n_s ** 3 / dt / 1e9, 4), "unit": "GFLOP/s", "cores": used,
             "kind": kind, "sample": f"{n_s}x{n_s} fp64 two-stage reduction, b={band}, {dt:.2f} s, "
                                     f"{used} OpenMP threads",
-            "threads": used, "host": hc,
+            "threads": used, "host": hc, "cores_note": cores_note,
             "sizes_s": {str(n): round(t, 3) for n, t in pts},
             "extrapolated": {"n": gpu_n, "seconds": round(t_ext, 1),
                              "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_ext / 1e9, 4),
                              "basis": "least-squares c*n^3 + d*n^2 (relative error) over the sampled sizes "
                                       + ",".join(str(n) for n, _ in pts) + "; NOT measured",
-                             "note": ("samples <= 1024 only: the LESS conservative fit (a 2048-inclusive "
-                                      "fit gave 2,421 s at 8192 in profiles/r02_cpu_baseline.json); "
-                                      "--cpu-n 320,640,1024,2048 adds the 2048 sample (~40 s)")
+                             "note": ("samples <= 1024 only: the LESS conservative fit (the default "
+                                      "--cpu-n 320,640,1024,2048 adds the 2048 sample, ~40 s)")
                              if max(n for n, _ in pts) < 2048 else "2048-inclusive fit"}}
 
 

@@ -110,7 +110,8 @@ int brd_check_errors(void);
  * HBM staging buffer of host-pointer calls, the stage-2 error word (read
  * first: BRD_EHIP if it was set).  brd_check_errors() visits every stream the
  * library has launched on, so call this before destroying such a stream.
- * Host-pointer calls free a staging buffer above 256 MiB on return. */
+ * Host-pointer calls keep their staging buffer until then (with
+ * BRD_STAGE_KEEP_MB set, one larger than that many MiB is freed on return). */
 int brd_release_stream(void *hip_stream);
 
 /* Per-kernel device timing for roofline reporting.  While enabled, the library

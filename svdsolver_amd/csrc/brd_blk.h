@@ -131,7 +131,8 @@ constexpr long kQS = (long)kCW * kCT;   // column stride of Q1 in the workspace 
 #ifndef BRD_HANDOFF_RELAXED
 #define BRD_HANDOFF_RELAXED 0   // 1: the relaxed (guide-measured) form of the prep / read-pass hand-offs (A/B)
 #endif
-constexpr int kBlkMaxRanks = 16;   // the blocked distributed path's most ranks (gathered row panel blocks)
+constexpr int kBlkMaxRanks = 16;   // the blocked distributed path's most ranks (the tail's nranks b <= kRmax)
+constexpr int kCqrRec = 1032;      // doubles per rank record: a 32 x 32 Gram, its exponent (128-B lines)
 struct CqrArgs {
     const void *src; long si, st;     // P(i, t) = src[i*si + t*st]
     int M;
@@ -144,16 +145,22 @@ struct CqrArgs {
     int azero;                        // 1: zeros into the panel's rows >= 32 (apan); 0: the caller zeroes
     double *qcopy;                    // optional copy of Q_t (1024 doubles, row-major) and the zero-panel
                                       // flag (element 1024): the distributed path's broadcast (null: none)
-    long blk, bstride;                // blk > 0: the source is stored in blocks of blk rows (a multiple of
-                                      // kCT), block q at src + q bstride, row i of it at (i mod blk) si
-                                      // (the distributed path's gathered [rank][32][slot] row panel)
-    int nreal[kBlkMaxRanks];          // blk > 0: real (not zero-padded) rows of block q; rows
-                                      // i mod blk >= nreal[i / blk] are padding and stay zero in Q
+    // The distributed row panel (blk_ge2band_dist): this rank's rows only,
+    // the panel-wide Grams from per-rank records all-gathered between the
+    // kernels.  rec null: the whole panel is here (one GPU).
+    double *rec;                      // record banks [3][nrec][kCqrRec]: G1 (+ exponent), G2, G3
+    int nrec, rme;                    // ranks, this rank's record
+    int *rctr;                        // 3 arrival counters (self-resetting): the last workgroup of a
+                                      // kernel sums the partials into this rank's record
+    long Mg;                          // the panel's rows over all ranks (the sCQR3 shift)
+    long goff;                        // this rank's first row in the panel (completion vectors)
+    int top;                          // 1: rows 0..31 here are the panel's top block (its R' and LU);
+                                      // 0: every row here is below it (zeroed in apan from row 0)
 };
 
 // scratch (doubles): three slots of Gram partials [kCW][1024] (two used), the
 // per-workgroup exponents, R1, the shifted-pass flag, and Q1 [32][kCW kCT]
-__host__ __device__ constexpr size_t cqr_ws_doubles() {
+__host__ __device__ constexpr size_t cqr_ws_doubles() {   // gp3: the distributed middle pass
     return (size_t)3 * 1024 * kCW + kCW + 2048 + 4 + (size_t)kCW * kCT * 32;
 }
 // Q_t (qt) and the zero flag are read by the next read pass's finishing
@@ -161,9 +168,9 @@ __host__ __device__ constexpr size_t cqr_ws_doubles() {
 __host__ __device__ constexpr size_t cqr_ws_qt() { return (size_t)3 * 1024 * kCW + kCW + 1024; }
 __host__ __device__ constexpr size_t cqr_ws_zero() { return cqr_ws_qt() + 1024 + 2; }
 struct CqrWs {
-    double *gp1, *gp2, *ew, *r1, *qt, *shifted, *zero, *q1;
+    double *gp1, *gp2, *gp3, *ew, *r1, *qt, *shifted, *zero, *q1;
     __device__ explicit CqrWs(double *ws)
-        : gp1(ws), gp2(ws + 1024 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
+        : gp1(ws), gp2(ws + 1024 * kCW), gp3(ws + 2048 * kCW), ew(ws + 3072 * kCW), r1(ws + 3072 * kCW + kCW),
           qt(ws + cqr_ws_qt()), shifted(ws + cqr_ws_qt() + 1024), zero(ws + cqr_ws_zero()),
           q1(ws + cqr_ws_zero() + 2) {}
 };
@@ -409,19 +416,18 @@ __device__ __forceinline__ u32x4_t rsrc_of(const void *base) {
                    0x00020000u};
 }
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-template <typename T> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+// AUX: the cache-policy bits (gfx950: 1 sc0, 2 nt, 16 sc1)
+template <typename T, int AUX = 0> __device__ __forceinline__ T buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, AUX));
+    else
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
 }
-template <> __device__ __forceinline__ float buf_ld<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-template <typename T> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ void buf_st<float>(float v, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
-}
-template <> __device__ __forceinline__ void buf_st<double>(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, 0);
+template <typename T, int AUX = 0> __device__ __forceinline__ void buf_st(T v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    if constexpr (sizeof(T) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0, AUX);
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, AUX);
 }
 
 // ---- launches ----------------------------------------------------------------
@@ -452,7 +458,7 @@ template <typename T>
 void launch_k_vsum(const T *vpart, T *vout, int nvirt, T *pbase, long pstride, const double *sgn, hipStream_t s);
 template <typename T>
 void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s);
-enum CqrKernel { kCqrGram, kCqrQ1, kCqrV, kCqrVInline };
+enum CqrKernel { kCqrGram, kCqrQ1, kCqrV, kCqrVInline, kCqrMid };
 template <typename T>
 void launch_k_cqr(CqrKernel which, int nwg, const CqrArgs &a, const FinArgs &f, hipStream_t s);
 template <typename T>
@@ -460,9 +466,6 @@ void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, dou
 // the distributed path's data movement (brd_blk_comm.hip)
 template <typename T>
 void launch_dist_unpack_v(const T *src, T *dst, int M, hipStream_t s);
-template <typename T>
-void launch_dist_scatter_u(const T *Vg, long base, int nc, T *RwT, long ldr, int rrow, long lcs, T *Ub, T *A, long lda,
-                           int c, int z0, hipStream_t s);
 template <typename T>
 void launch_dist_psum(const T *part, int ks, long mp, int rows, T *buf, hipStream_t s);
 

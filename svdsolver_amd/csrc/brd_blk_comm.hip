@@ -1,5 +1,5 @@
 // Blocked stage 1 sharded over P GPUs (brd_stage1_blk.hip, blk_ge2band_dist):
-// the data-movement kernels around its three collectives per panel.  All are
+// the data-movement kernels around its collectives.  All are
 // HBM-bound copies of m x 32 or n_loc x 32 panels (one read + one write per
 // element, 16-byte accesses along the 32 columns of a row).
 #include "brd_blk.h"
@@ -15,23 +15,6 @@ __global__ void __launch_bounds__(256) k_dist_unpack_v(const T *__restrict__ src
     const long e = (long)blockIdx.x * 256 + threadIdx.x;   // one 2-element pair
     const long row = e >> 4, p = e & 15;
     if (row < M) *(v2 *)(dst + row * 256 + 2 * p) = *(const v2 *)(src + row * 32 + 2 * p);
-}
-
-// This rank's rows of the gathered LQ basis (rotated order, rows [base, base +
-// nc) of Vg [..][32]) into RwT rows rrow .. rrow + 31 at local columns lcs ..
-// and into Ub (the X pass's B operand, [col][32]); the row panel's entries of
-// A (rows c .. c + 31) at those columns zeroed from local item z0 on (the
-// band block's owner keeps its first 32: k_cqr_v wrote the band block there).
-template <typename T>
-__global__ void __launch_bounds__(256) k_dist_scatter_u(const T *__restrict__ Vg, long base, int nc, T *__restrict__ RwT,
-                                                        long ldr, int rrow, long lcs, T *__restrict__ Ub,
-                                                        T *__restrict__ A, long lda, int c, int z0) {
-    const int il = blockIdx.x * 8 + (threadIdx.x >> 5), t = threadIdx.x & 31;
-    if (il >= nc) return;
-    const T v = Vg[(base + il) * 32 + t];
-    RwT[(long)(rrow + t) * ldr + lcs + il] = v;
-    Ub[(lcs + il) * 32 + t] = v;
-    if (il >= z0) A[(long)(c + t) * lda + lcs + il] = (T)0;
 }
 
 // The X pass's split-K partials (part [ks][mp][32], rows [0, rows)) summed in
@@ -54,13 +37,6 @@ void launch_dist_unpack_v(const T *src, T *dst, int M, hipStream_t s) {
                dim3(256), s, src, dst, M);
 }
 template <typename T>
-void launch_dist_scatter_u(const T *Vg, long base, int nc, T *RwT, long ldr, int rrow, long lcs, T *Ub, T *A, long lda,
-                           int c, int z0, hipStream_t s) {
-    if (nc <= 0) return;
-    blk_launch("s1_comm", 0.0, 32.0 * nc * 4 * sizeof(T), k_dist_scatter_u<T>, dim3((unsigned)((nc + 7) / 8)), dim3(256),
-               s, Vg, base, nc, RwT, ldr, rrow, lcs, Ub, A, lda, c, z0);
-}
-template <typename T>
 void launch_dist_psum(const T *part, int ks, long mp, int rows, T *buf, hipStream_t s) {
     if (rows <= 0) return;
     const long el = (long)rows * 32;
@@ -70,8 +46,6 @@ void launch_dist_psum(const T *part, int ks, long mp, int rows, T *buf, hipStrea
 
 #define BRD_INST(T)                                                                                         \
     template void launch_dist_unpack_v<T>(const T *, T *, int, hipStream_t);                                \
-    template void launch_dist_scatter_u<T>(const T *, long, int, T *, long, int, long, T *, T *, long, int,  \
-                                           int, hipStream_t);                                               \
     template void launch_dist_psum<T>(const T *, int, long, int, T *, hipStream_t);
 BRD_INST(double)
 BRD_INST(float)

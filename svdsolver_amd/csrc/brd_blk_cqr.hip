@@ -189,7 +189,7 @@ __device__ __forceinline__ void umul_row(double (&x)[32], const double (&Ri)[32]
 #ifndef BRD_GRAM_BATCH
 #define BRD_GRAM_BATCH 8    // partials per batch of loads in flight (A/B knob, tools/variant_lib.sh)
 #endif
-__device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg) {
+__device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg, long gs = 1024) {
     const int tid = threadIdx.x;
     constexpr int GB = BRD_GRAM_BATCH;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -199,7 +199,7 @@ __device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const 
         for (int k = 0; k < GB; ++k) {
             const int kc = min(k0 + k, nwg - 1);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[k][u] = gp[(size_t)kc * 1024 + tid + kCT * u];
+            for (int u = 0; u < 4; ++u) v[k][u] = gp[(size_t)kc * gs + tid + kCT * u];
         }
 #pragma unroll
         for (int k = 0; k < GB; ++k) {
@@ -220,8 +220,7 @@ template <typename T>
 __device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x)[32]) {
     const T *src = (const T *)a.src;
     const int ic = i < a.M ? i : 0;
-    const T *srow = a.blk > 0 ? src + (size_t)(ic / a.blk) * a.bstride + (size_t)(ic % a.blk) * a.si
-                              : src + (size_t)ic * a.si;
+    const T *srow = src + (size_t)ic * a.si;
     if (a.st == 1) {   // a row of 32 contiguous elements: 16-byte loads
         typedef typename G2<T>::v2 v2;
 #pragma unroll
@@ -243,7 +242,9 @@ __device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x
 
 // Gram partial of the workgroup's rows (one per thread) -> dst (1024 doubles):
 // the four waves' partials summed in fixed order
-__device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32], double *dst) {
+// (coh: agent-scope stores, for the distributed form's last-arriver sum in
+// the same kernel, cqr_to_record)
+__device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32], double *dst, bool coh = false) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double gacc[3][4] = {};
     gram_wave(L, w, lane, x, gacc);
@@ -261,22 +262,84 @@ __device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32
     __syncthreads();
     for (int el = tid; el < 1024; el += kCT) {
         const int i = el >> 5, t = el & 31;
-        dst[el] = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
+        const double v = (gw[0][i][t] + gw[1][i][t]) + (gw[2][i][t] + gw[3][i][t]);
+        if (coh) __hip_atomic_store(dst + el, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else     dst[el] = v;
     }
 }
 
 // the panel's exponent e (INT_MIN: the panel is zero) and the partials' scale
 // factors 2^(2 (e_k - e)) into L.scl
-__device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg, bool ones) {
+__device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg, bool ones, long es = 1) {
     const int tid = threadIdx.x;
     __shared__ int ewl[kCW];
-    if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[tid] : INT_MIN;
+    if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[(size_t)tid * es] : INT_MIN;
     __syncthreads();
     int e = INT_MIN;
     for (int k = 0; k < nwg; ++k) e = max(e, ewl[k]);
     if (tid < kCW) L.scl[tid] = ones ? 1.0 : ((tid < nwg && ewl[tid] != INT_MIN) ? ldexp(1.0, 2 * (ewl[tid] - e)) : 0.0);
     __syncthreads();
     return e;
+}
+
+// ---- the distributed form (CqrArgs::rec): per-rank records ------------------
+// The last workgroup of a kernel to arrive sums the kernel's partials (gp
+// [nwg][1024], agent-scope stores; exponents ew, or none) in fixed order into
+// this rank's record of bank `bank`: the 32 x 32 Gram of this rank's rows
+// (scaled by 2^-2e_r) and e_r.  The caller all-gathers the bank; the next
+// kernel sums the nrec records in rank order (cqr_gram_src), so every rank
+// holds the same panel-wide Gram, bit for bit.
+__device__ __forceinline__ double *cqr_bank(const CqrArgs &a, int bank) {
+    return a.rec + (size_t)bank * a.nrec * kCqrRec;
+}
+__device__ void cqr_to_record(CqrLds &L, const CqrArgs &a, const double *gp, const double *ew, int bank) {
+    const int tid = threadIdx.x, nwg = gridDim.x;
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's partial stores have landed
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(a.rctr + bank, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == nwg - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(a.rctr + bank, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ int ewl[kCW];
+    if (tid < kCW)
+        ewl[tid] = (ew && tid < nwg) ? (int)__hip_atomic_load(ew + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : INT_MIN;
+    __syncthreads();
+    int e = INT_MIN;
+    if (ew)
+        for (int k = 0; k < nwg; ++k) e = max(e, ewl[k]);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < nwg; ++k) {
+        const double sk = !ew ? 1.0 : (ewl[k] == INT_MIN ? 0.0 : ldexp(1.0, 2 * (ewl[k] - e)));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            acc[u] = fma(sk, __hip_atomic_load(gp + (size_t)k * 1024 + tid + kCT * u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT), acc[u]);
+    }
+    double *r = cqr_bank(a, bank) + (size_t)a.rme * kCqrRec;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[tid + kCT * u] = acc[u];
+    if (tid == 0) r[1024] = (double)e;
+}
+// the panel-wide Gram's source: the records of bank `bank` (distributed) or
+// this kernel's own partials
+struct GramSrc {
+    const double *gp, *ew;
+    int n;
+    long gs, es;
+};
+__device__ __forceinline__ GramSrc cqr_gram_src(const CqrArgs &a, int bank, const double *gp, const double *ew) {
+    if (a.rec) {
+        const double *b = cqr_bank(a, bank);
+        return GramSrc{b, b + 1024, a.nrec, kCqrRec, kCqrRec};
+    }
+    return GramSrc{gp, ew, (int)gridDim.x, 1024, 1};
 }
 
 template <typename T>
@@ -303,25 +366,31 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
 #pragma unroll
         for (int t = 0; t < 32; ++t) x[t] = ldexp(x[t], -e_w);
     }
-    cqr_gram_partial(L, x, W.gp1 + (size_t)wg * 1024);
-    if (tid == 0) W.ew[wg] = (double)e_w;
+    const bool coh = a.rec != nullptr;
+    cqr_gram_partial(L, x, W.gp1 + (size_t)wg * 1024, coh);
+    if (tid == 0) {
+        if (coh) __hip_atomic_store(W.ew + wg, (double)e_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else     W.ew[wg] = (double)e_w;
+    }
+    if (coh) cqr_to_record(L, a, W.gp1, W.ew, 0);
 }
 
 template <typename T>
 __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     __shared__ CqrLds L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x;
     CqrWs W(a.ws);
     if (tid == 0) L.flags = 0;
     const int i = wg * kCT + tid;
     double x[32];
     cqr_load_row<T>(a, i, x);   // in flight under the Gram sum and the Cholesky
-    const int e = cqr_exponent(L, W.ew, nwg, false);
+    const GramSrc g1 = cqr_gram_src(a, 0, W.gp1, W.ew);
+    const int e = cqr_exponent(L, g1.ew, g1.n, false, g1.es);
     if (e == INT_MIN) {   // zero panel: k_cqr_v writes V = [I; 0], T = 0, R = 0
         if (wg == 0 && tid == 0) W.shifted[0] = 0.0;
         return;
     }
-    gram_sum_all(L, W.gp1, L.scl, nwg);
+    gram_sum_all(L, g1.gp, L.scl, g1.n, g1.gs);
     __syncthreads();
     if (w == 0) {
         bool good = chol_wave(L.g, L.r1, L.r1w, lane);
@@ -333,7 +402,7 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
             double tr = 0;
 #pragma unroll
             for (int k = 0; k < 32; ++k) tr += L.g[k][k];
-            const double sh = 11.0 * (32.0 * a.M + 32.0 * 33.0) * 0x1p-53 * tr;
+            const double sh = 11.0 * (32.0 * (a.rec ? a.Mg : a.M) + 32.0 * 33.0) * 0x1p-53 * tr;
             if (lane < 32) L.g[lane][lane] += sh;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -358,7 +427,8 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < 32; ++t) W.q1[t * kQS + i] = x[t];
-    cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024);
+    cqr_gram_partial(L, x, W.gp2 + (size_t)wg * 1024, a.rec != nullptr);
+    if (a.rec) cqr_to_record(L, a, W.gp2, nullptr, 1);
 }
 
 // After a shifted first pass only (W.shifted): sCQR3's middle pass, run by
@@ -419,13 +489,6 @@ __device__ __attribute__((noinline)) bool chol_def(const double (&G)[32][kSP], d
     return chol_wave<true>(G, R, Rw, lane, mask);
 }
 
-// a zero-padded row of the distributed path's gathered row panel (CqrArgs::nreal)
-__device__ __forceinline__ bool cqr_pad_row(const CqrArgs &a, int i) {
-    if (a.blk <= 0) return false;
-    const int q = (int)(i / a.blk);
-    return q < kBlkMaxRanks && (int)(i - q * a.blk) >= a.nreal[q];
-}
-
 __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, const CqrArgs &a, int nwg, double (&x)[32]) {
     const int M = a.M;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -449,13 +512,9 @@ __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, cons
 #pragma unroll
         for (int t = 0; t < 32; ++t) y[t] = W.q1[t * kQS + i];
         if (mask) {   // (chol_wave<true> made the solve leave these columns alone)
-            // padding rows keep their zero: a completion there would give Q
-            // rows the caller drops (k_dist_scatter_u), and the kept rows of Q
-            // would not be orthonormal
-            const bool pad = cqr_pad_row(a, i);
 #pragma unroll
             for (int t = 0; t < 32; ++t)
-                if (mask >> t & 1u) y[t] = pad ? 0.0 : cqr_completion(i, t, cscale);
+                if (mask >> t & 1u) y[t] = cqr_completion(i, t, cscale);
         }
         trsm_row(y, L.r2w);
         if (i >= M) {
@@ -514,6 +573,109 @@ __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, cons
     gram_collect(L, L.g, gacc);
 }
 
+// The distributed form's sCQR3 middle pass (CqrArgs::rec; on one GPU
+// k_cqr_v runs it inside, walking all rows: cqr_shifted_pass).  After a
+// shifted first pass: R~ = chol(G2) from the records (deficient columns
+// marked, chol_def), this rank's rows of y = Q1 R~^-1 (completion vectors in
+// the deficient columns) back into Q1's place, and y's Gram into bank 2.
+// Every rank launches it (the collective after it is unconditional); an
+// unshifted panel returns at once and bank 2 is not read.
+template <typename T>
+__global__ void __launch_bounds__(kCT, 1) k_cqr_mid(CqrArgs a) {
+    __shared__ CqrLds L;
+    __shared__ unsigned dmask;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = blockIdx.x * kCT + tid;
+    CqrWs W(a.ws);
+    if (W.shifted[0] == 0.0) return;
+    if (tid == 0) L.flags = 0;
+    if (tid < kCW) L.scl[tid] = 1.0;
+    double y[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) y[t] = W.q1[t * kQS + i];
+    __syncthreads();
+    gram_sum_all(L, cqr_bank(a, 1), L.scl, a.nrec, kCqrRec);
+    __syncthreads();
+    if (w == 0) {
+        unsigned mk = 0;
+        const bool good = chol_def(L.g, L.r2, L.r2w, lane, &mk);
+        if (lane == 0) {
+            if (!good) L.flags = 1;
+            dmask = mk;
+        }
+    }
+    __syncthreads();
+    const unsigned mask = dmask;
+    if (mask) {
+        const double cscale = 1.0 / sqrt((double)max(a.Mg, 1L));
+#pragma unroll
+        for (int t = 0; t < 32; ++t)
+            if (mask >> t & 1u) y[t] = cqr_completion((int)(i + a.goff), t, cscale);
+    }
+    trsm_row(y, L.r2w);
+    if (i >= a.M) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) y[t] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 32; ++t) W.q1[t * kQS + i] = y[t];
+    if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cqr_gram_partial(L, y, W.gp3 + (size_t)blockIdx.x * 1024, true);
+    cqr_to_record(L, a, W.gp3, nullptr, 2);
+}
+
+// k_cqr_v's shifted path in the distributed form: R~ again from G2 (the same
+// records, the same factor as k_cqr_mid's), R~ R1 into L.r1, and the final
+// Gram from bank 2 (x: this thread's row of y, k_cqr_mid).  With deficient
+// columns, Ra = chol(Gram(y)) and x <- x Ra^-1, Ra R~' R1 into L.r1, and the
+// final Gram taken as I: one pass fewer than cqr_shifted_pass (whose final
+// Gram would need a fourth collective), so Q's orthogonality there is one
+// CholeskyQR pass's on y, ~ cond(y)^2 u.
+__device__ __attribute__((noinline)) void cqr_shifted_dist(CqrLds &L, const CqrWs &W, const CqrArgs &a, double (&x)[32]) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = blockIdx.x * kCT + tid;
+    __shared__ unsigned dmask;
+    gram_sum_all(L, cqr_bank(a, 1), L.scl, a.nrec, kCqrRec);
+    __syncthreads();
+    if (w == 0) {
+        unsigned mk = 0;
+        const bool good = chol_def(L.g, L.r2, L.r2w, lane, &mk);
+        if (lane == 0) {
+            if (!good) L.flags = 1;
+            dmask = mk;
+        }
+    }
+    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
+    __syncthreads();
+    const unsigned mask = dmask;
+    gram_sum_all(L, cqr_bank(a, 2), L.scl, a.nrec, kCqrRec);
+    __syncthreads();
+    if (mask) {
+        if (w == 0) {
+            const bool good = chol_wave(L.g, L.u, L.mm, lane);
+            if (lane == 0 && !good) L.flags = 1;
+        }
+        __syncthreads();
+        trsm_row(x, L.mm);
+        if (i >= a.M) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) x[t] = 0.0;
+        }
+    }
+    const int ti = w >> 1, tj = w & 1;
+    for (int pass = 0; pass < (mask ? 2 : 1); ++pass) {
+        Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
+        if (tj >= ti) rt = tile_mm(pass ? L.u : L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
+            L.r1[i2][c] = i2 <= c ? rt[g] : 0.0;
+        }
+        __syncthreads();
+    }
+    if (mask)
+        for (int el = tid; el < 1024; el += kCT) L.g[el >> 5][el & 31] = (el >> 5) == (el & 31) ? 1.0 : 0.0;
+}
+
 // INLINE (the last LQ panel of a block, whose U's top block the block update
 // reads straight away): workgroup 0 also runs cqr_finish itself and patches
 // V's top block to Q_t - S in place.
@@ -523,7 +685,8 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
     CqrWs W(a.ws);
     if (tid == 0) L.flags = 0;
-    const int e = cqr_exponent(L, W.ew, nwg, true);
+    const GramSrc g1 = cqr_gram_src(a, 0, W.gp1, W.ew);
+    const int e = cqr_exponent(L, g1.ew, g1.n, true, g1.es);   // (L.scl: ones)
     const bool zero = e == INT_MIN;   // V = [I; 0], T = 0, R = 0
     const int i = wg * kCT + tid;
     T *ap = (T *)a.apan;
@@ -531,13 +694,17 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     T *vd2 = (T *)a.vdst2;
     double x[32];
     const bool sh = !zero && W.shifted[0] != 0.0;
-    if (!zero && !sh) {   // this thread's row of Q1, in flight under the Gram sum
+    if (!zero && (!sh || a.rec)) {   // this thread's row of Q1 (or y), in flight under the Gram sum
 #pragma unroll
         for (int t = 0; t < 32; ++t) x[t] = W.q1[t * kQS + i];
     }
     if (!zero) {
-        if (sh) cqr_shifted_pass(L, W, a, nwg, x);
-        else    gram_sum_all(L, W.gp2, L.scl, nwg);
+        if (sh && a.rec) cqr_shifted_dist(L, W, a, x);
+        else if (sh)     cqr_shifted_pass(L, W, a, nwg, x);
+        else {
+            const GramSrc g2 = cqr_gram_src(a, 1, W.gp2, nullptr);
+            gram_sum_all(L, g2.gp, L.scl, g2.n, g2.gs);
+        }
         __syncthreads();
         // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
         // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
@@ -624,13 +791,14 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     store_v(x, 0, INT_MAX);   // V' = Q (the top rows get - S after the LU: k_vsum)
     if (a.azero) {   // zeros below the panel's R block
         typedef typename G2<T>::v2 v2;
+        const int zlo = a.top ? 32 : 0;
         if (a.ast == 1) {
 #pragma unroll 4
             for (int it = 0; it < 16; ++it) {
                 const int row = wrow0 + 4 * it + (lane >> 4), cp = 2 * (lane & 15);
-                if (row >= 32 && row < a.M) *(v2 *)(ap + (size_t)row * a.asi + cp) = v2{(T)0, (T)0};
+                if (row >= zlo && row < a.M) *(v2 *)(ap + (size_t)row * a.asi + cp) = v2{(T)0, (T)0};
             }
-        } else if (i >= 32 && i < a.M) {
+        } else if (i >= zlo && i < a.M) {
             T *arow = ap + (size_t)i * a.asi;
 #pragma unroll
             for (int t = 0; t < 32; ++t) arow[t * a.ast] = (T)0;
@@ -653,7 +821,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         }
         if (tid == 0) a.qcopy[1024] = zero ? 1.0 : 0.0;
     }
-    if (w == 3 && ap) {
+    if (w == 3 && ap && a.top) {
         if (!sh)   // (after a shifted pass L.r1 already holds R R1)
             for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -695,6 +863,7 @@ void launch_k_cqr(CqrKernel which, int nwg, const CqrArgs &a, const FinArgs &f, 
         case kCqrGram: blk_launch("s1_cqr", 0.0, 0.0, k_cqr_gram<T>, dim3(nwg), dim3(kCT), s, a); break;
         case kCqrQ1:   blk_launch("s1_cqr", 0.0, 0.0, k_cqr_q1<T>, dim3(nwg), dim3(kCT), s, a); break;
         case kCqrV:    blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, false>, dim3(nwg), dim3(kCT), s, a, f); break;
+        case kCqrMid:  blk_launch("s1_cqr", 0.0, 0.0, k_cqr_mid<T>, dim3(nwg), dim3(kCT), s, a); break;
         default:       blk_launch("s1_cqr", 0.0, 0.0, k_cqr_v<T, true>, dim3(nwg), dim3(kCT), s, a, f); break;
     }
 }

@@ -167,6 +167,11 @@ __device__ __forceinline__ void vmw(int n) {
 #define BRD_BLKUPD_CSPREAD 1
 #endif
 
+#ifndef BRD_BLKUPD_CPOL
+#define BRD_BLKUPD_CPOL 2   // cache policy of k_blkupd_p's C loads and stores: nt (streamed once;
+                            // keeps L2 for the Lw / RwT strips: s1_blkupd 12.80 -> 12.57 ms at N = 8192 fp64)
+#endif
+constexpr int kCPol = BRD_BLKUPD_CPOL;
 template <typename T>
 __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     typedef typename Mf<T>::v4 v4;
@@ -332,11 +337,11 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
                 if (have_prev) {
 #pragma unroll
                     for (int e = c * EPC; e < (c + 1) * EPC; ++e)
-                        buf_st<T>(cbuf[e >> 3][(e >> 2) & 1][e & 3], cprev.r, c_at(cprev, e >> 3, (e >> 2) & 1, e & 3));
+                        buf_st<T, kCPol>(cbuf[e >> 3][(e >> 2) & 1][e & 3], cprev.r, c_at(cprev, e >> 3, (e >> 2) & 1, e & 3));
                 }
 #pragma unroll
                 for (int e = c * EPC; e < (c + 1) * EPC; ++e)
-                    cbuf[e >> 3][(e >> 2) & 1][e & 3] = buf_ld<T>(ccur.r, c_at(ccur, e >> 3, (e >> 2) & 1, e & 3));
+                    cbuf[e >> 3][(e >> 2) & 1][e & 3] = buf_ld<T, kCPol>(ccur.r, c_at(ccur, e >> 3, (e >> 2) & 1, e & 3));
             }
             chunk_mma(c % kBR, BRD_BLKUPD_CAFTER ? 1 : 0);
         }
@@ -356,7 +361,7 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) buf_st<T>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
+                for (int g = 0; g < 4; ++g) buf_st<T, kCPol>(cbuf[i][j][g], cprev.r, c_at(cprev, i, j, g));
     }
     if (a.nh == 0) return;
     // The last round in half tiles (launch_k_blkupd: when it holds at most

@@ -32,45 +32,123 @@ struct S2Ring {
     __device__ __forceinline__ T *row(int r) const { return d + slot(r) * P + 31 - r; }
 };
 
-// Apply the reflector of x (x[0] the pivot, every lane holds all N) to the
-// lane's vector a (the same arithmetic for both window kinds):
-//   |x|^2 and sigma = sum_{j>=1} a_j x_j in four chains each,
-//   rn = 1/|x|, u1 = x0 - s |x|, alpha = 1/u1, tau = -s u1 / |x|,
-//   dot = a0 + alpha sigma, a0 -= tau dot, a_j -= tau dot alpha x_j.
+// ---- lag-2 schedule: the deferred corner (k_sweeps) --------------------------
+// Window t of sweep i+1 may start once sweep i has finished window t+2: the
+// only element it shares with window t+3 of sweep i is its own bottom-right
+// corner, which is never in its source row / column
+// (tests/test_stage2_schedule.py::test_lag2_corner_rule_preserves_serial_order).
+// So a full window defers its LAST lane (right window: its last row; left
+// window: its last column), whose dot product involves the corner: that lane
+// neither updates nor stores, and keeps sigma' (its a . x without the corner
+// term) for the next window of the same sweep.  The next window holds the
+// deferred vector as element 31 of its lanes 0..31 (right -> left: row
+// r + 63 is the left window's last row; left -> right: column r' + 63 is the
+// right window's last column), the deferred vector's pivot as lane 0's
+// element 31 and the corner as lane 31's; once sweep i has finished window
+// t+3 (the next window's own lag-2 condition) it completes the update there
+// (s2_fixup) before its own reflector, in the same arithmetic as an
+// undeferred lane (bitwise the result the lag-3 order gives).
+template <typename T>
+struct S2Fix {
+    T sig;     // sigma' of the deferred lane (sum over j = 1 .. 30 of a_j x_j)
+    T alpha;   // the deferring window's reflector: w_j = alpha x_j (j >= 1), w_0 = 1
+    T tau;
+    T x31;     // x_31 (the corner's factor)
+};
+
+__device__ __forceinline__ double s2_readlane(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float s2_readlane(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Apply the reflector of x (x[0] the pivot, every lane holds all N = 32) to
+// the lane's vector a (the same arithmetic for both window kinds):
+//   |x|^2 and sigma' = sum_{j=1..30} a_j x_j in four chains each,
+//   sigma = sigma' + a_31 x_31, rn = 1/|x|, u1 = x0 - s |x|, alpha = 1/u1,
+//   tau = -s u1 / |x|, dot = a0 + alpha sigma, a0 -= tau dot,
+//   a_j -= tau dot alpha x_j.
+// Returns sigma' (and the scalars in f) for a deferred lane.
 template <typename T, int N>
-__device__ __forceinline__ void s2_refl(T (&a)[N], const T (&x)[N]) {
+__device__ __forceinline__ T s2_refl(T (&a)[N], const T (&x)[N], S2Fix<T> &f) {
+    static_assert(N == 32, "b = 32 windows");
     T q0 = x[0] * x[0], q1 = (T)0, q2 = (T)0, q3 = (T)0;
     T g0 = (T)0, g1 = (T)0, g2 = (T)0, g3 = (T)0;
 #pragma unroll
-    for (int j = 1; j < N; j += 4) {
+    for (int j = 1; j < N - 1; j += 4) {
         q1 = fma(x[j], x[j], q1);
         g1 = fma(a[j], x[j], g1);
-        if (j + 1 < N) { q2 = fma(x[j + 1], x[j + 1], q2); g2 = fma(a[j + 1], x[j + 1], g2); }
-        if (j + 2 < N) { q3 = fma(x[j + 2], x[j + 2], q3); g3 = fma(a[j + 2], x[j + 2], g3); }
-        if (j + 3 < N) { q0 = fma(x[j + 3], x[j + 3], q0); g0 = fma(a[j + 3], x[j + 3], g0); }
+        if (j + 1 < N - 1) { q2 = fma(x[j + 1], x[j + 1], q2); g2 = fma(a[j + 1], x[j + 1], g2); }
+        if (j + 2 < N - 1) { q3 = fma(x[j + 2], x[j + 2], q3); g3 = fma(a[j + 2], x[j + 2], g3); }
+        if (j + 3 < N - 1) { q0 = fma(x[j + 3], x[j + 3], q0); g0 = fma(a[j + 3], x[j + 3], g0); }
     }
+    q0 = fma(x[N - 1], x[N - 1], q0);
     const T qq = (q0 + q1) + (q2 + q3);
-    const T sig = (g0 + g1) + (g2 + g3);
+    const T sigp = (g0 + g1) + (g2 + g3);
+    const T sig = fma(a[N - 1], x[N - 1], sigp);
     const T rn = rsq_nr(qq);
     const T nrm = qq * rn;
     const T sgn = x[0] >= (T)0 ? (T)-1 : (T)1;
     const T u1 = fma(-sgn, nrm, x[0]);
     const T alpha = rcp_nr(u1);
     const T tau = -sgn * u1 * rn;
+    // (explicit fma everywhere: s2_fixup repeats this arithmetic for a
+    // deferred lane and must round exactly alike -- a contraction the compiler
+    // chose differently in the two places would change the result)
     const T dot = fma(alpha, sig, a[0]);
-    const T td = tau * dot;
-    const T tda = td * alpha;
-    a[0] -= td;
+    const T tda = (tau * dot) * alpha;
+    a[0] = fma(-tau, dot, a[0]);
 #pragma unroll
     for (int j = 1; j < N; ++j) a[j] = fma(-tda, x[j], a[j]);
+    f.alpha = alpha;
+    f.tau = tau;
+    f.x31 = x[N - 1];
+    return sigp;
 }
+
+// Complete the previous window's deferred vector: element 31 of lanes 0..31
+// (lane 0: its pivot, lane 31: the corner, now final).  The pivot is this
+// window's x[31] as loaded and the corner comes from its own broadcast load,
+// so the reflector scalars and x[31]'s new value (the pivot's) need no
+// cross-lane reads of the window's data; xs: the deferring window's source
+// vector (LDS, 32 elements).
+template <typename T, int N>
+__device__ __forceinline__ void s2_fixup(T (&a)[N], T (&x)[N], const S2Fix<T> &f, const T *xs, T corner, int lane) {
+    const T a0 = x[N - 1];
+    const T dot = fma(f.alpha, fma(corner, f.x31, f.sig), a0);
+    const T tda = (f.tau * dot) * f.alpha;
+    const T p = fma(-f.tau, dot, a0);   // the pivot's new value (lane 0's element 31)
+    if (lane < 32) a[N - 1] = lane == 0 ? p : fma(-tda, xs[lane], a[N - 1]);
+    x[N - 1] = p;
+}
+
+// What a window does around its reflector (k_sweeps):
+//   fix   the previous window was deferred: complete it (s2_fixup) and store
+//         its 32 elements, then publish the sweep's progress (prog = t, front)
+//   defer this window is deferred: its last lane keeps its vector (no
+//         update, no store), fo receives the fixup data, xs the source vector
+struct S2Pub {
+    int *prog, *front;
+    int prog_v, front_v;
+    __device__ __forceinline__ void publish(int lane) const {
+        asm volatile("" ::: "memory");   // LDS executes a wave's operations in order
+        if (lane == 0) {
+            __hip_atomic_store(front, front_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(prog, prog_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+};
 
 // Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
 // j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
 // reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
 // nc = 32 (no predicates).
 template <typename T, bool FULL>
-__device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane) {
+__device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
+                                            bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo, T *xs,
+                                            const S2Pub &pub) {
     constexpr int N = 32;
     const bool rok = FULL || lane < nr;
     const T *px = rg.row(i1) + j1;
@@ -82,8 +160,20 @@ __device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1,
         x[j] = cok ? px[j] : (T)0;
         a[j] = (cok && rok) ? pa[j] : (T)0;
     }
-    s2_refl<T, N>(a, x);
-    if (rok) {
+    if (fix) {   // the deferred column j1 + 31 of rows i1 .. i1 + 31
+        s2_fixup<T, N>(a, x, fi, xs, rg.row(i1 + 31)[j1 + 31], lane);
+        if (lane < 32) pa[N - 1] = a[N - 1];
+        pub.publish(lane);
+    }
+    const T sigp = s2_refl<T, N>(a, x, fo);
+    if (defer) {
+        fo.sig = s2_readlane(sigp, 63);
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) xs[j] = x[j];
+        }
+    }
+    if (rok && !(defer && lane == 63)) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
             if (FULL || j < nc) pa[j] = a[j];
@@ -95,7 +185,9 @@ __device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1,
 // Rows that do not wrap the ring sit P - 1 elements apart: one base address
 // and immediate offsets.
 template <typename T, bool FULL>
-__device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane) {
+__device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
+                                           bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo, T *xs,
+                                           const S2Pub &pub) {
     constexpr int N = 32;
     const bool cok = FULL || lane < nc;
     const int q = cok ? lane : 0;
@@ -109,8 +201,20 @@ __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, 
             x[j] = rk ? bx[j * (rg.P - 1)] : (T)0;
             a[j] = (rk && cok) ? bx[j * (rg.P - 1) + q] : (T)0;
         }
-        s2_refl<T, N>(a, x);
-        if (cok) {
+        if (fix) {   // the deferred row i1 + 31 of columns j1 .. j1 + 31
+            s2_fixup<T, N>(a, x, fi, xs, bx[(N - 1) * (rg.P - 1) + 31], lane);
+            if (lane < 32) bx[(N - 1) * (rg.P - 1) + q] = a[N - 1];
+            pub.publish(lane);
+        }
+        const T sigp = s2_refl<T, N>(a, x, fo);
+        if (defer) {
+            fo.sig = s2_readlane(sigp, 63);
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) xs[j] = x[j];
+            }
+        }
+        if (cok && !(defer && lane == 63)) {
 #pragma unroll
             for (int j = 0; j < N; ++j)
                 if (FULL || j < nr) bx[j * (rg.P - 1) + q] = a[j];
@@ -126,8 +230,20 @@ __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, 
             x[j] = rk ? rows[j][0] : (T)0;
             a[j] = (rk && cok) ? rows[j][q] : (T)0;
         }
-        s2_refl<T, N>(a, x);
-        if (cok) {
+        if (fix) {
+            s2_fixup<T, N>(a, x, fi, xs, rows[N - 1][31], lane);
+            if (lane < 32) rows[N - 1][q] = a[N - 1];
+            pub.publish(lane);
+        }
+        const T sigp = s2_refl<T, N>(a, x, fo);
+        if (defer) {
+            fo.sig = s2_readlane(sigp, 63);
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) xs[j] = x[j];
+            }
+        }
+        if (cok && !(defer && lane == 63)) {
 #pragma unroll
             for (int j = 0; j < N; ++j)
                 if (FULL || j < nr) rows[j][q] = a[j];

@@ -174,9 +174,10 @@ template <typename T>
 static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, long vsi, long vst, T *vdst2, long vsi2,
                              long vst2, T *tout, T *apan, long asi, long ast, char *ws, const BlkLayout &Ly, int *err,
                              hipStream_t s, bool inl, const FinArgs &fin, int azero = 1, double *qcopy = nullptr,
-                             long blk = 0, long bstride = 0, bool gram_done = false, const int *nreal = nullptr) {
+                             bool gram_done = false) {
     CqrArgs a;
-    for (int q = 0; q < kBlkMaxRanks; ++q) a.nreal[q] = nreal ? nreal[q] : 0;
+    a.rec = nullptr; a.nrec = 1; a.rme = 0; a.rctr = nullptr;
+    a.Mg = M; a.goff = 0; a.top = 1;
     a.src = src; a.si = si; a.st = st; a.M = M;
     a.vdst = vdst; a.vsi = vsi; a.vst = vst;
     a.vdst2 = vdst2; a.vsi2 = vsi2; a.vst2 = vst2;
@@ -187,7 +188,6 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
     a.err = err;
     a.azero = azero;
     a.qcopy = qcopy;
-    a.blk = blk; a.bstride = bstride;
     if (!gram_done) launch_k_cqr<T>(kCqrGram, nwg, a, fin, s);   // else the prep kernel formed gp1 / ew
     launch_k_cqr<T>(kCqrQ1, nwg, a, fin, s);
     launch_k_cqr<T>(inl ? kCqrVInline : kCqrV, nwg, a, fin, s);
@@ -264,7 +264,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
-                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq, 1, nullptr, 0, 0, fold_qr);
+                                  A + (size_t)c * lda + c, lda, 1, ws, Ly, err, s, false, fq, 1, nullptr, fold_qr);
             }
             if (e != hipSuccess) return e;
             // ---- Y pass (+ the QR panel's finish) + LQ of the row panel -------
@@ -293,7 +293,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             const FinArgs fl = fin_of(sgl + 32 * j, Sj, A + (size_t)c * lda + c + 32, 1, lda);
             e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, n2, RwT + (size_t)(128 + 32 * j) * ldr + c + 32, 1, ldr,
                               Ub + (size_t)(c + 32) * 32, 32, 1, Sj, A + (size_t)c * lda + c + 32, 1, lda, ws, Ly, err, s,
-                              inl, fl, 1, nullptr, 0, 0, fold_lq);
+                              inl, fl, 1, nullptr, fold_lq);
             if (e != hipSuccess) return e;
             // ---- X pass (+ the LQ panel's finish) --------------------------------
             bool xfold = false;
@@ -375,27 +375,15 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 // ==========================================================================
 namespace {
 struct DistBlk {
-    size_t bc, gat, vg, ar, total;
-    long cnt;   // rows per all-gather slot, at most (the first panel)
+    size_t bc, rec, ar, total;
 };
-// rows per all-gather slot for the row panel of global panel p: the most
-// trailing columns any rank holds, rounded up to a workgroup of the panel QR
-// (so every slot starts at a workgroup boundary)
-long dist_slot_rows(int n, int P, int p) {
-    int nmax = 0;
-    for (int r = 0; r < P; ++r)
-        nmax = std::max(nmax, dist_local_cols(n, 32, P, r) - dist_panels_before(p + 1, P, r) * 32);
-    return std::max(256L, ((long)nmax + 255) / 256 * 256);
-}
 DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
     const BlkLayout Ly = blk_layout(m, std::max(dist_local_cols(n, 32, P, rank), 1), elem);
     DistBlk D;
-    D.cnt = dist_slot_rows(n, P, 0);
     size_t off = Ly.total;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     D.bc = take((size_t)m * 32 * elem + 1032 * sizeof(double));   // V' rows, then Q_t + zero flag
-    D.gat = take((size_t)2 * P * D.cnt * 32 * elem);              // gathered slots + rotation tail
-    D.vg = take((size_t)P * D.cnt * 32 * elem);                   // the gathered panel's basis
+    D.rec = take((size_t)3 * P * kCqrRec * sizeof(double));       // the row panel QR's Gram records
     D.ar = take(((size_t)m * 32 + 256 * 32) * elem);              // G (256 x 32), then X rows
     D.total = off;
     return D;
@@ -404,7 +392,7 @@ DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
 
 size_t blk_dist_ws_bytes(int m, int n, int P, int rank, size_t elem) { return dist_blk_layout(m, n, P, rank, elem).total; }
 bool blk_dist_fits(int n, int P) {
-    return P >= 1 && P <= kBlkMaxRanks && (long)P * dist_slot_rows(n, P, 0) <= (long)kCW * kCT;
+    return P >= 1 && P <= kBlkMaxRanks && dist_local_cols(n, 32, P, 0) <= kCW * kCT;   // rank 0 holds the most
 }
 
 #define BD_HIP(expr)                                                                          \
@@ -435,7 +423,8 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
     T *tf = (T *)(ws + Ly.tf);
     int *ctr = (int *)(ws + Ly.ctr);
     const long ldr = Ly.ldr;
-    T *bc = (T *)(ws + D.bc), *gat = (T *)(ws + D.gat), *Vg = (T *)(ws + D.vg), *ar = (T *)(ws + D.ar);
+    T *bc = (T *)(ws + D.bc), *ar = (T *)(ws + D.ar);
+    double *rec = (double *)(ws + D.rec);
     const int dt = sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32;
     BD_HIP(hipMemsetAsync(ctr, 0, 64 * sizeof(int), s));
     double *sgq = (double *)(ws + Ly.sg), *sgl = sgq + NBMAX * 32, *sg0 = sgq + 2 * NBMAX * 32;
@@ -451,6 +440,22 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         p.sgn = sgn; p.cc = cc; p.zfill = 0;
         return p;
     };
+    // the panel QR's first Gram partials formed by the prep kernel that
+    // writes the panel (no k_cqr_gram launch), as on one GPU (BRD_PREP_GRAM)
+    const int foldm = getenv("BRD_PREP_GRAM") ? atoi(getenv("BRD_PREP_GRAM")) : 3;
+    auto gram_into = [&](PrepArgs &pa) {
+        double *cw = (double *)(ws + Ly.cws);
+        pa.gram = 1;
+        pa.gpp = (double *)(ws + Ly.gpp);
+        pa.gout = cw;                    // CqrWs::gp1
+        pa.gew = cw + 3072 * kCW;        // CqrWs::ew
+        pa.gcnt = ctr + 64;
+    };
+    // The X partials the next prep reads: all-reduced into ar (P > 1), or the
+    // read pass's split-K partials themselves (one rank: no sum, no copy)
+    const void *xpart = ar + 256 * 32, *xG = ar;
+    long xmp = 0;
+    int xks = 1;
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
             const int p = k0 / 32 + j, c = 32 * p, mr = m - c, mx = m - c - 32;
@@ -461,20 +466,23 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             const int nc = n_loc - (int)lcs;                 // local trailing columns
             T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
             double *qt = (double *)((char *)bc + (size_t)mr * 32 * sizeof(T));   // Q_t, zero flag
-            const long cnt = dist_slot_rows(n, P, p);   // <= D.cnt
             // ---- X_{j-1} (every rank) + the column panel's QR (its owner) ----------
+            const bool fold_qr = own && j > 0 && (foldm & 1);
             if (j > 0) {
-                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1),
-                                   sg0, lco);
+                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, xpart, xmp, xks, xG, tf + 1024 * (NBMAX + j - 1), sg0, lco);
+                if (fold_qr) gram_into(pa);
                 launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
-            const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
+            // Q_t and the zero flag: broadcast with V' (P > 1), else where k_cqr_v left them
+            const double *qtp = P > 1 ? qt : cws + cqr_ws_qt(), *zp = P > 1 ? qt + 1024 : cws + cqr_ws_zero();
+            const FinArgs fq{qtp, zp, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
             if (own) {
                 const T *src = j == 0 ? A + (size_t)c * lda + lco : (const T *)(ws + Ly.qp);
                 const long si = j == 0 ? lda : 1, st = j == 0 ? 1 : Ly.mp;
-                BD_HIP(launch_cqr<T>(src, si, st, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, bc, 32, 1, Tj,
-                                     A + (size_t)c * lda + lco, lda, 1, ws, Ly, err, s, false, fq, 1, qt));
+                BD_HIP(launch_cqr<T>(src, si, st, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, P > 1 ? bc : nullptr, 32,
+                                     1, Tj, A + (size_t)c * lda + lco, lda, 1, ws, Ly, err, s, false, fq, 1,
+                                     P > 1 ? qt : nullptr, fold_qr));
             }
             if (P > 1) {
                 BD_TRY(C.bcast(bc, (size_t)mr * 32 * sizeof(T) + 1025 * sizeof(double), o, s));
@@ -485,46 +493,72 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             BD_HIP(launch_rpass<T>(true, A + (size_t)c * lda + lcs, lda, mr, nc, Lw + (size_t)c * 256 + 32 * j, 256,
                                    Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
                                    Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j));
-            // ---- the row panel: corrected locally, gathered, factored everywhere ----
-            T *slot = gat + (size_t)me * cnt * 32;
+            // ---- the row panel: corrected locally, factored by a sharded CholeskyQR --
+            const bool fold_lq = P == 1 && (foldm & 2);
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
-                pa.Qp = slot; pa.mq = cnt; pa.zfill = (int)cnt;   // [32][cnt]: coalesced, as on one GPU
+                if (fold_lq) gram_into(pa);
                 launch_k_prep<T>(true, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
-            if (P > 1) BD_TRY(C.allgather(slot, gat, (size_t)cnt * 32 * sizeof(T), s));
-            if (o2 != 0)   // rotate: panel p+1's slot first (its first 32 rows are the band block's columns)
-                BD_HIP(hipMemcpyAsync(gat + (size_t)P * cnt * 32, gat, (size_t)o2 * cnt * 32 * sizeof(T),
-                                      hipMemcpyDeviceToDevice, s));
-            const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
-                             own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
-            int nreal[kBlkMaxRanks] = {};   // block q of the rotated panel: rank (o2 + q) mod P's trailing columns
-            for (int q = 0; q < P && q < kBlkMaxRanks; ++q) {
-                const int r = (o2 + q) % P;
-                nreal[q] = std::max(0, dist_local_cols(n, 32, P, r) - dist_panels_before(p + 1, P, r) * 32);
+            if (P == 1) {   // one rank: the whole row panel is here (no records, no middle pass)
+                const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj, A + (size_t)c * lda + lcs, 1,
+                                 lda};
+                BD_HIP(launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, nc, RwT + (size_t)(128 + 32 * j) * ldr + lcs, 1,
+                                     ldr, Ub + (size_t)lcs * 32, 32, 1, Sj, A + (size_t)c * lda + lcs, 1, lda, ws, Ly,
+                                     err, s, true, fl, 1, nullptr, fold_lq));
+            } else {
+                CqrArgs a;
+                a.src = ws + Ly.qp; a.si = 1; a.st = Ly.mp; a.M = std::max(nc, 0);
+                a.vdst = RwT + (size_t)(128 + 32 * j) * ldr + lcs; a.vsi = 1; a.vst = ldr;
+                a.vdst2 = Ub + (size_t)lcs * 32; a.vsi2 = 32; a.vst2 = 1;
+                a.tout = Sj;
+                a.apan = A + (size_t)c * lda + lcs; a.asi = 1; a.ast = lda;
+                a.ws = (double *)(ws + Ly.cws);
+                a.err = err;
+                a.azero = 1;
+                a.qcopy = nullptr;
+                a.rec = rec; a.nrec = P; a.rme = me; a.rctr = ctr + 40;
+                a.Mg = n - c - 32;
+                a.goff = (long)((me - o2 + P) % P) * kCW * kCT;
+                a.top = own2 ? 1 : 0;
+                const int nwg = std::max(1, (a.M + kCT - 1) / kCT);
+                const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
+                                 own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
+                const size_t rb = (size_t)kCqrRec * sizeof(double);
+                launch_k_cqr<T>(kCqrGram, nwg, a, fl, s);   // -> record bank 0: this rank's G1, exponent
+                if (P > 1) BD_TRY(C.allgather(rec + (size_t)me * kCqrRec, rec, rb, s));
+                launch_k_cqr<T>(kCqrQ1, nwg, a, fl, s);     // R1 (every rank, the same), Q1 rows -> bank 1
+                if (P > 1) BD_TRY(C.allgather(rec + (size_t)(P + me) * kCqrRec, rec + (size_t)P * kCqrRec, rb, s));
+                launch_k_cqr<T>(kCqrMid, nwg, a, fl, s);    // sCQR3's middle pass (shifted panels) -> bank 2
+                if (P > 1)
+                    BD_TRY(C.allgather(rec + (size_t)(2 * P + me) * kCqrRec, rec + (size_t)2 * P * kCqrRec, rb, s));
+                // V rows into RwT and Ub; the top block's owner finishes inline (LU, S_j, the band block)
+                launch_k_cqr<T>(own2 ? kCqrVInline : kCqrV, nwg, a, fl, s);
+                BD_HIP(hipGetLastError());
+                if (P > 1) BD_TRY(C.bcast(Sj, 1024 * sizeof(T), o2, s));
             }
-            BD_HIP(launch_cqr<T>(gat + (size_t)o2 * cnt * 32, 1, cnt, (int)(P * cnt), Vg, 32, 1, nullptr, 0, 0, Sj,
-                                 own2 ? A + (size_t)c * lda + lcs : nullptr, 1, lda, ws, Ly, err, s, true, fl, 0,
-                                 nullptr, cnt, cnt * 32, false, nreal));
-            launch_dist_scatter_u<T>(Vg, (long)((me - o2 + P) % P) * cnt, nc, RwT, ldr, 128 + 32 * j, lcs, Ub, A, lda,
-                                     c, own2 ? 32 : 0, s);
             // ---- X pass (local columns), partials summed and all-reduced ------------
             if (nc > 0) {
                 int ks_x = 1;
                 BD_HIP(launch_rpass<T>(false, A + (size_t)(c + 32) * lda + lcs, lda, nc, mx, Ub + lcs * 32, 32,
                                        RwT + lcs, ldr, ws, Ly, ctr + 16, err, s, target, &ks_x, nullptr, nullptr, 0,
                                        nullptr, ar));
-                launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
+                if (P > 1) {
+                    launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
+                } else {
+                    xpart = ws + Ly.part; xmp = Ly.mp; xks = ks_x;
+                }
             } else {
                 BD_HIP(hipMemsetAsync(ar, 0, ((size_t)mx * 32 + 256 * 32) * sizeof(T), s));
+                xpart = ar + 256 * 32; xmp = 0; xks = 1;
             }
             if (P > 1) BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32, dt, s));
         }
         // ---- block end: X_3 (every rank), the rank-256 update of my columns ---------
         const int k1 = k0 + NBMAX * 32;
         {
-            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
+            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, xpart, xmp, xks, xG, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
             launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
             BD_HIP(hipGetLastError());
         }

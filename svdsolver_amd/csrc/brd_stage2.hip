@@ -1198,6 +1198,15 @@ namespace brd {
 //  * a compact role split (no SGPR spills: one window code path per kind).
 // ==========================================================================
 constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
+#ifndef BRD_S2_LAG2
+#define BRD_S2_LAG2 0                 // 1: lag 2 with the deferred corner (A/B; bitwise the same band,
+                                      // measured 93 ms against lag 3's 72 ms at N = 8192 fp64: the
+                                      // fixup's extra LDS round trip sits on the chain it shortens)
+#endif
+constexpr bool kS2Lag2 = BRD_S2_LAG2 != 0;
+#ifndef BRD_S2_DEFER_LAG2
+#define BRD_S2_DEFER_LAG2 1           // 0: deferred windows still wait for lag 3 (A/B of the fixup alone)
+#endif
 struct SweepFlags {
     int prog[12];    // tasks completed per compute wave
     int front[12];   // top row of each compute wave's next window (n when done)
@@ -1267,6 +1276,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
     T *ring = (T *)smem;
     const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
     SweepFlags *F = (SweepFlags *)(smem + ring_bytes);
+    T *xsc = (T *)(smem + ring_bytes + ((sizeof(SweepFlags) + 15) & ~(size_t)15));   // S x 32: deferring windows' x
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const S2Ring<T> rg{ring, P, R, magic};
     const int nbundles = (n - 1 + S - 1) / S;
@@ -1293,44 +1303,63 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
 
         if (wave < nsw) {
             // ---------------- compute wave: sweep i0 + wave ----------------
+            // Lag 2 with the deferred corner (brd_s2win.h): a full window whose
+            // next window can host the fixup starts once the previous sweep has
+            // finished window t+2 and defers its last lane; any other window
+            // keeps lag 3.  prog[wave] = t means windows < t are complete,
+            // deferred parts included (published after the fixup).
             const int i = i0 + wave;
             SweepIter it;
             it.init(n, n, b, i, sigma);
             const int prev_ntask = wave > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
+            T *xs = xsc + 32 * wave;
+            S2Fix<T> fx{(T)0, (T)0, (T)0, (T)0};
+            bool pend = false;
             for (int t = 0; t < it.ntask; ++t) {
                 bool right;
                 const Win w = it.task(t, right);
+                const int nr = w.i2 - w.i1, nc = w.j2 - w.j1;
+                const bool live = nr > 0 && nc > 0;
+                const bool full = live && (right ? (nr == 2 * b && nc == b) : (nr == b && nc == 2 * b));
+                bool defer = false;
+                if (full && t + 1 < it.ntask && kS2Lag2) {
+                    SweepIter it2 = it;
+                    bool rn;
+                    const Win wn = it2.task(t + 1, rn);
+                    defer = wn.i2 - wn.i1 >= b && wn.j2 - wn.j1 >= b;
+                }
                 int spins = 0;
                 TRT(beta, wave, t, 0);
-                if (wave > 0) {   // lag 3 against the previous sweep (tests/test_stage2_schedule.py)
-                    const int need = min(t + 4, prev_ntask);
+                if (wave > 0) {
+                    const int need = min(t + (defer ? 4 - BRD_S2_DEFER_LAG2 : 4), prev_ntask);
                     while (lds_ld(&F->prog[wave - 1]) < need) {
                         __builtin_amdgcn_s_sleep(0);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 12); break; }
                     }
                 }
-                const int nr = w.i2 - w.i1, nc = w.j2 - w.j1;
                 TRT(beta, wave, t, 1);
-                if (nr > 0 && nc > 0) {
+                if (live) {
                     while (lds_ld(&F->loaded) < w.i2) {
                         __builtin_amdgcn_s_sleep(0);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 13); break; }
                     }
                     TRT(beta, wave, t, 2);
                     asm volatile("" ::: "memory");
+                    const S2Pub pub{&F->prog[wave], &F->front[wave], t, w.i1};
+                    S2Fix<T> fo;
                     if (right) {
-                        if (nr == 2 * b && nc == b) s2_right_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane);
-                        else                        s2_right_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane);
+                        if (full) s2_right_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
+                        else      s2_right_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
                     } else {
-                        if (nr == b && nc == 2 * b) s2_left_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane);
-                        else                        s2_left_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane);
+                        if (full) s2_left_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
+                        else      s2_left_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
                     }
+                    if (defer) fx = fo;
                     asm volatile("" ::: "memory");
                 }
+                pend = defer;
                 TRT(beta, wave, t, 3);
-                // LDS executes this wave's operations in order: the window's ring
-                // stores land before these words.
-                if (lane == 0) {
+                if (!defer && lane == 0) {   // LDS in order: the window's ring stores land first
                     lds_st(&F->front[wave], it.next_top(t));
                     lds_st(&F->prog[wave], t + 1);
                 }
@@ -1630,8 +1659,9 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
 // (tuning).
 constexpr int kSweepSlack = 40;
 template <typename T>
-static size_t sweeps_lds_bytes(int R) {
-    return (((size_t)R * ring_pitch<T>(32) * sizeof(T) + 15) & ~(size_t)15) + sizeof(SweepFlags);
+static size_t sweeps_lds_bytes(int R, int S) {
+    return (((size_t)R * ring_pitch<T>(32) * sizeof(T) + 15) & ~(size_t)15) + ((sizeof(SweepFlags) + 15) & ~(size_t)15) +
+           (kS2Lag2 ? (size_t)S * 32 * sizeof(T) : 0);
 }
 template <typename T>
 static bool sweeps_plan(int n, int &S, int &R) {
@@ -1642,9 +1672,9 @@ static bool sweeps_plan(int n, int &S, int &R) {
     if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
     for (S = std::min(smax, std::max(1, n - 1)); S >= 1; --S) {
         const int rmin = ring_min_rows(32, S) + kSweepSlack;
-        if (sweeps_lds_bytes<T>(rmin) <= budget) {
+        if (sweeps_lds_bytes<T>(rmin, S) <= budget) {
             R = rmin;
-            while (R < n + 1 && sweeps_lds_bytes<T>(R + 1) <= budget) ++R;
+            while (R < n + 1 && sweeps_lds_bytes<T>(R + 1, S) <= budget) ++R;
             return true;
         }
     }
@@ -1682,7 +1712,7 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         const dim3 block(64 * (S + 2 + kSweepWriters));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
         const void *fn = (const void *)k_sweeps<T>;
-        const size_t lds = sweeps_lds_bytes<T>(R);
+        const size_t lds = sweeps_lds_bytes<T>(R, S);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         const int cap = coresident_limit(fn, (int)block.x, lds);

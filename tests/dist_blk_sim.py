@@ -12,9 +12,12 @@ j (global panel p, column c):
   1. the owner of p corrects its column panel, CholeskyQR -> V_j, T_j, R;
      BROADCAST of V_j, T_j;
   2. Y pass on this rank's trailing columns (local);
-  3. this rank's columns of the corrected row panel; ALL-GATHER, rotated so
-     that rank (p+1) mod P (panel p+1: the band block's columns) comes first;
-     every rank factors the gathered panel (identical U, S), keeps its rows;
+  3. this rank's columns of the corrected row panel, factored by a sharded
+     CholeskyQR2 (cholqr_dist): per pass a local 32 x 32 Gram, ALL-GATHER of
+     the per-rank Grams summed in rank order (every rank: the same R), local
+     Q = P R^-1; the rank holding the band block's columns (panel p+1, rank
+     (p+1) mod P: the top block of the panel) finishes the basis-kernel
+     reconstruction and BROADCASTS S_j;
   4. X pass partial over this rank's columns (with its part of the Y^T U,
      U^T U corrections); ALL-REDUCE;
 block end: the rank-2 nb b update of this rank's trailing columns (local).
@@ -23,6 +26,59 @@ import numpy as np
 
 from dist_sim import ge2band_dist_sim, panels_before
 from s1_model import blocked_columns, cholqr_house
+
+
+def cholqr_dist(Ploc, top, root, P, dist, group=None, iters=2):
+    """The row panel's QR with its rows sharded over the ranks (this rank's
+    rows Ploc; `top`: this rank holds the panel's first k rows): CholeskyQR2
+    with all-gathered per-rank Grams, then the basis-kernel form of the
+    Householder reconstruction (Ballard et al. 2015; the GPU kernels'
+    k_cqr_v): V = Q - [S; 0], T = -S (U^-1 L^-1)^T with Q_t - S = L U, the
+    band block S R.  Returns this rank's rows of V, T (broadcast from the
+    top rank) and, on the top rank, S R."""
+    import torch
+    nc, k = Ploc.shape
+    mx = torch.tensor([float(np.max(np.abs(Ploc))) if Ploc.size else 0.0], dtype=torch.float64)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    scale = float(mx[0])
+    if scale == 0.0:
+        V = np.zeros((nc, k))
+        if top:
+            V[:k, :k] = np.eye(k)
+        return V, np.zeros((k, k)), np.zeros((k, k))
+    e = np.floor(np.log2(scale))
+    Q = Ploc * 2.0 ** (-e)
+    R = np.eye(k)
+    for _ in range(iters):
+        parts = [torch.zeros((k, k), dtype=torch.float64) for _ in range(P)]
+        dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(Q.T @ Q)), group=group)
+        G = parts[0].numpy().copy()
+        for r in range(1, P):
+            G = G + parts[r].numpy()
+        C = np.linalg.cholesky(G).T          # upper, G = C^T C: the same on every rank
+        Q = np.linalg.solve(C.T, Q.T).T
+        R = C @ R
+    R = R * 2.0 ** e
+    tb = np.zeros((k, k))
+    Rh = np.zeros((k, k))
+    V = Q.copy()
+    if top:   # the modified LU of the top block: s_j = -sign(pivot)
+        lu = Q[:k].copy()
+        S = np.zeros(k)
+        for j in range(k):
+            s = -1.0 if lu[j, j] >= 0 else 1.0
+            S[j] = s
+            lu[j, j] -= s
+            lu[j + 1:, j] /= lu[j, j]
+            lu[j + 1:, j + 1:] -= np.outer(lu[j + 1:, j], lu[j, j + 1:])
+        L1 = np.tril(lu, -1) + np.eye(k)
+        U = np.triu(lu)
+        tb = -np.diag(S) @ np.linalg.inv(L1 @ U).T
+        V[:k] -= np.diag(S)
+        Rh = np.triu(np.diag(S) @ R)
+    t = torch.from_numpy(tb)
+    dist.broadcast(t, src=root, group=group)
+    return V, t.numpy(), Rh
 
 
 def global_columns(n, b, P, rank):
@@ -65,16 +121,9 @@ def ge2band_blk_dist_sim(A_loc, n, b, rank, P, dist, group=None, nb=4):
             Yf = np.zeros((n_loc, b))
             Yf[tr] = (A_loc[c:, tr].T @ Vj - Y[tr] @ (V[c:].T @ Vj) - U[tr] @ (X[c:].T @ Vj)) @ Tj
             V = np.hstack([V, Vf]); Y = np.hstack([Y, Yf])
-            # 3. the row panel: local columns, gathered (padded slots), factored everywhere
+            # 3. the row panel: local columns, a sharded CholeskyQR
             Q = A_loc[c:c + b, tr] - V[c:c + b] @ Y[tr].T - X[c:c + b] @ U[tr].T
-            cnt = max(1, max(int((global_columns(n, b, P, r) >= c + b).sum()) for r in range(P)))
-            slot = np.zeros((cnt, b)); slot[:nc] = Q.T
-            parts = [torch.zeros((cnt, b), dtype=torch.float64) for _ in range(P)]
-            dist.all_gather(parts, torch.from_numpy(slot), group=group)
-            Qg = np.concatenate([parts[(o2 + s) % P].numpy() for s in range(P)])
-            Ug, Sj, Lt = cholqr_house(Qg)
-            pos = (rank - o2) % P
-            Uj = Ug[pos * cnt:pos * cnt + nc]
+            Uj, Sj, Lt = cholqr_dist(Q.T, rank == o2, o2, P, dist, group)
             A_loc[c:c + b, tr] = 0.0
             if rank == o2:
                 lc2 = panels_before(p + 1, P, rank) * b

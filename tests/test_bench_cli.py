@@ -71,3 +71,25 @@ def test_bench_two_ranks_end_to_end():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["n"] == 1024
     assert d["config"]["matrices_per_timed_region"] == 3
+
+
+@pytest.mark.gpu
+def test_bench_eight_ranks_end_to_end():
+    """bench.py --gpus 8 as the driver launches it on an 8-GPU node (configs[4]'s
+    P = 8 layout: 8 ranks x the lanes' communicators), rehearsed on one GPU
+    through the host-callback communicator at n = 2048 (the blocked path with
+    the sharded row-panel CholeskyQR)."""
+    import json
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "8", "--comm", "host", "--size", "2048", "--steps", "2", "--warmup", "1",
+           "--lanes", "2", "--cpu-baseline", "off"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["value"] > 0 and d["config"]["n"] == 2048
+    assert d["config"]["matrices_per_timed_region"] == 2

@@ -117,7 +117,7 @@ def _blk_sim_worker(rank, world, port, n, b, seed, out_path):
     tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 512), (3, 600), (4, 704)])
+@pytest.mark.parametrize("world,n", [(2, 512), (3, 600), (4, 704), (8, 640)])
 def test_blocked_distributed_algorithm_gloo(world, n, tmp_path):
     """The blocked distributed stage 1's data flow (tests/dist_blk_sim.py:
     owner-side column-panel QR + broadcast, local Y pass, gathered row panel
@@ -199,6 +199,10 @@ def _gpu_worker(rank, world, port, n, b, dtype, mode, out_path, root=0):
     (3, 1100, 32, np.float64, "host"),
     (4, 1024, 32, np.float64, "host"),
     (1, 1024, 32, np.float64, "rccl"),
+    # the P = 8 layout of configs[4]: 8 ranks on the blocked
+    # path with the sharded row-panel CholeskyQR, and a ragged tail
+    (8, 2048, 32, np.float64, "host"),
+    (8, 2096, 32, np.float64, "host"),
 ])
 def test_distributed_stage1_gpu(world, n, b, dtype, mode, tmp_path):
     """Against the single-GPU stage 1 (|band|, fp64 1e-12): with b = 32 in

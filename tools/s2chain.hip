@@ -87,8 +87,11 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
             else       win_left_full<T, B>(acc, i1, i1, lane);
         } else if constexpr (MODE == 2) {
             const S2Ring<T> rg{ring, P, R, magic};
-            if (right) s2_right_w1<T, true>(rg, i1, i1 + 32, 64, 32, lane);
-            else       s2_left_w1<T, true>(rg, i1, i1, 32, 64, lane);
+            S2Fix<T> fi{}, fo;
+            const S2Pub pub{prog + 30, prog + 31, 0, 0};
+            T *xs = (T *)(xr + 16);
+            if (right) s2_right_w1<T, true>(rg, i1, i1 + 32, 64, 32, lane, false, fi, false, fo, xs, pub);
+            else       s2_left_w1<T, true>(rg, i1, i1, 32, 64, lane, false, fi, false, fo, xs, pub);
         } else {
             const S2Ring<T> rg{ring, P, R, magic};
             S2Pair pr{xr + W * sw, pw, t + 1};

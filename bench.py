@@ -305,13 +305,13 @@ def rpass_roofline(rp, dtype, n):
 
 
 def stage2_roofline(sw, n, b, dtype, steps):
-    """Stage 2 (k_band2bd_bundle, one launch per step): every bundle of sweeps
+    """Stage 2 (k_sweeps, one launch per step): every bundle of sweeps
     streams the band rows below its first sweep in and out once (P = 3b
     elements per row), so the algorithmic HBM bytes are 2 * P * sizeof(T) *
     sum over bundles of the rows; the kernel is bound by its chain of
     dependent windows (about 4 per sweep), not by HBM (Stage 2)."""
     esz = 8 if dtype == "f64" else 4
-    S = 3 if dtype == "f64" else 5      # sweeps per bundle (brd_stage2.hip bundle_plan)
+    S = 3 if dtype == "f64" else 7      # sweeps per bundle (brd_stage2.hip sweeps_plan)
     P = 3 * b
     # minimum: the band (3b stored diagonals per row: the fill of a bulge
     # reaches b-1 below and 2b-1 above the diagonal) read once, written once
@@ -323,8 +323,8 @@ def stage2_roofline(sw, n, b, dtype, steps):
     # per launch (one launch per reduction; in the multi-GPU pipeline rank 0
     # runs the sweeps of only the matrices whose index is 0 mod world)
     ms = sw["ms"] / max(sw.get("launches", steps), 1)
-    traffic, src = pmc_traffic(n, dtype, "void brd::k_band2bd_bundle<" + ("double" if dtype == "f64" else "float"))
-    return {"kernel": "k_band2bd_bundle (stage-2 sweeps)", "bound": "latency (dependent window chain)",
+    traffic, src = pmc_traffic(n, dtype, "void brd::k_sweeps<" + ("double" if dtype == "f64" else "float"))
+    return {"kernel": "k_sweeps (stage-2 sweeps)", "bound": "latency (dependent window chain)",
             "ms": round(ms, 3),
             "minimum_bytes": round(minimum), "streamed_bytes_by_design": round(streamed),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,

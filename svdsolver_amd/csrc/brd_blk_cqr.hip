@@ -577,7 +577,11 @@ __device__ __forceinline__ void cqr_shifted_pass(CqrLds &L, const CqrWs &W, cons
 // k_cqr_v runs it inside, walking all rows: cqr_shifted_pass).  After a
 // shifted first pass: R~ = chol(G2) from the records (deficient columns
 // marked, chol_def), this rank's rows of y = Q1 R~^-1 (completion vectors in
-// the deficient columns) back into Q1's place, and y's Gram into bank 2.
+// the deficient columns) back into Q1's place, y's Gram into bank 2, and
+// R~ R1 into R1's place (workgroup 0); k_cqr_v then runs its usual final
+// pass on y with the Gram from bank 2.  (With deficient columns that is one
+// CholeskyQR pass on y where cqr_shifted_pass makes two -- a third Gram would
+// need a fourth collective -- so Q's orthogonality there is ~ cond(y)^2 u.)
 // Every rank launches it (the collective after it is unconditional); an
 // unshifted panel returns at once and bank 2 is not read.
 template <typename T>
@@ -619,61 +623,20 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_mid(CqrArgs a) {
 #pragma unroll
     for (int t = 0; t < 32; ++t) W.q1[t * kQS + i] = y[t];
     if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cqr_gram_partial(L, y, W.gp3 + (size_t)blockIdx.x * 1024, true);
-    cqr_to_record(L, a, W.gp3, nullptr, 2);
-}
-
-// k_cqr_v's shifted path in the distributed form: R~ again from G2 (the same
-// records, the same factor as k_cqr_mid's), R~ R1 into L.r1, and the final
-// Gram from bank 2 (x: this thread's row of y, k_cqr_mid).  With deficient
-// columns, Ra = chol(Gram(y)) and x <- x Ra^-1, Ra R~' R1 into L.r1, and the
-// final Gram taken as I: one pass fewer than cqr_shifted_pass (whose final
-// Gram would need a fourth collective), so Q's orthogonality there is one
-// CholeskyQR pass's on y, ~ cond(y)^2 u.
-__device__ __attribute__((noinline)) void cqr_shifted_dist(CqrLds &L, const CqrWs &W, const CqrArgs &a, double (&x)[32]) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = blockIdx.x * kCT + tid;
-    __shared__ unsigned dmask;
-    gram_sum_all(L, cqr_bank(a, 1), L.scl, a.nrec, kCqrRec);
-    __syncthreads();
-    if (w == 0) {
-        unsigned mk = 0;
-        const bool good = chol_def(L.g, L.r2, L.r2w, lane, &mk);
-        if (lane == 0) {
-            if (!good) L.flags = 1;
-            dmask = mk;
-        }
-    }
-    for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
-    __syncthreads();
-    const unsigned mask = dmask;
-    gram_sum_all(L, cqr_bank(a, 2), L.scl, a.nrec, kCqrRec);
-    __syncthreads();
-    if (mask) {
-        if (w == 0) {
-            const bool good = chol_wave(L.g, L.u, L.mm, lane);
-            if (lane == 0 && !good) L.flags = 1;
-        }
+    if (blockIdx.x == 0) {   // R~ R1 (waves 0-3: one 16 x 16 tile each) into R1's place
+        for (int el = tid; el < 1024; el += kCT) L.r1[el >> 5][el & 31] = W.r1[el];
         __syncthreads();
-        trsm_row(x, L.mm);
-        if (i >= a.M) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) x[t] = 0.0;
-        }
-    }
-    const int ti = w >> 1, tj = w & 1;
-    for (int pass = 0; pass < (mask ? 2 : 1); ++pass) {
+        const int ti = w >> 1, tj = w & 1;
         Mf<double>::v4 rt = {0.0, 0.0, 0.0, 0.0};
-        if (tj >= ti) rt = tile_mm(pass ? L.u : L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
-        __syncthreads();
+        if (tj >= ti) rt = tile_mm(L.r2, L.r1, ti, tj, lane, 16 * ti, 32);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int i2 = 16 * ti + Mf<double>::crow(lane >> 4, g), c = 16 * tj + (lane & 15);
-            L.r1[i2][c] = i2 <= c ? rt[g] : 0.0;
+            W.r1[i2 * 32 + c] = i2 <= c ? rt[g] : 0.0;
         }
-        __syncthreads();
     }
-    if (mask)
-        for (int el = tid; el < 1024; el += kCT) L.g[el >> 5][el & 31] = (el >> 5) == (el & 31) ? 1.0 : 0.0;
+    cqr_gram_partial(L, y, W.gp3 + (size_t)blockIdx.x * 1024, true);
+    cqr_to_record(L, a, W.gp3, nullptr, 2);
 }
 
 // INLINE (the last LQ panel of a block, whose U's top block the block update
@@ -699,10 +662,10 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         for (int t = 0; t < 32; ++t) x[t] = W.q1[t * kQS + i];
     }
     if (!zero) {
-        if (sh && a.rec) cqr_shifted_dist(L, W, a, x);
-        else if (sh)     cqr_shifted_pass(L, W, a, nwg, x);
-        else {
-            const GramSrc g2 = cqr_gram_src(a, 1, W.gp2, nullptr);
+        if (sh && !a.rec) {
+            cqr_shifted_pass(L, W, a, nwg, x);
+        } else {   // (distributed, shifted: x = y and its Gram in bank 2, k_cqr_mid)
+            const GramSrc g2 = cqr_gram_src(a, sh ? 2 : 1, W.gp2, nullptr);
             gram_sum_all(L, g2.gp, L.scl, g2.n, g2.gs);
         }
         __syncthreads();
@@ -822,7 +785,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         if (tid == 0) a.qcopy[1024] = zero ? 1.0 : 0.0;
     }
     if (w == 3 && ap && a.top) {
-        if (!sh)   // (after a shifted pass L.r1 already holds R R1)
+        if (!sh || a.rec)   // (after a one-GPU shifted pass L.r1 already holds R R1)
             for (int el = lane; el < 1024; el += 64) L.r1[el >> 5][el & 31] = zero ? 0.0 : W.r1[el];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

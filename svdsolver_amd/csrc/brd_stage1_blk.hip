@@ -357,21 +357,27 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 //        (modified LU, T_j, signs) beside its own Y pass, which is local:
 //        Y_j = A^T V_j T_j needs only this rank's columns (svd_cuda_2.cu:1184,
 //        qr_apply_cuda's column loop, sharded by columns).
-//   LQ   every rank corrects its columns of the row panel (k_prep_lq) into
-//        its slot ([32][slot rows], transposed as on one GPU) of an ALL-GATHER
-//        (slots padded to a multiple of 256 rows: a panel-QR workgroup's rows
-//        lie in one slot);
-//        every rank runs the same CholeskyQR on the gathered panel, rotated
-//        so that panel p+1's columns (the band block, on rank (p+1) mod P)
-//        come first, and finishes inline -- identical U_j, S_j everywhere;
-//        each rank keeps its rows of U_j (k_dist_scatter_u).
+//   LQ   every rank corrects its columns of the row panel (k_prep_lq) and
+//        factors its rows of the panel's transpose by a SHARDED CholeskyQR
+//        (lq_cuda, svd_cuda_2.cu:959, does the same QR on
+//        one device): per pass a local 32 x 32 Gram (k_cqr_gram / k_cqr_q1 /
+//        k_cqr_mid: the kernel's last workgroup sums its partials into this
+//        rank's record), an ALL-GATHER of the P records (8 KB each), summed
+//        in rank order by every rank -- the same R on every rank, bit for bit
+//        -- and the local Q = P R^-1; three all-gathers per panel (G1, G2 and
+//        sCQR3's middle Gram).  The rank holding panel p+1 (the band block's
+//        columns: the panel's top block) finishes the basis-kernel
+//        reconstruction inline (LU of Q_t - S, S_j, the band block) and
+//        BROADCASTS S_j (32 x 32).  U_j's rows stay where they were formed.
 //   X    X_j = A U_j S_j sums over columns: each rank's split-K partials
 //        (and its part of G = Rw^T U_j) are summed locally (k_dist_psum) and
 //        ALL-REDUCED (m - c - 32 + 256 rows of 32).
-// Message sizes per panel: m x 32 (broadcast), n x 32 in total (all-gather),
-// (m + 256) x 32 (all-reduce) -- against the per-panel path's m x b
-// broadcast + P b^2 gather + b x m all-reduce, but 2.5 passes over the
-// trailing matrix per 32 columns instead of 4, the update on the matrix cores.
+// Message sizes per panel: m x 32 (broadcast), 3 x P x 8 KB (all-gathers),
+// 8 KB (broadcast of S_j), (m + 256) x 32 (all-reduce) -- against the
+// per-panel path's m x b broadcast + P b^2 gather + b x m all-reduce, but 2.5
+// passes over the trailing matrix per 32 columns instead of 4, the update on
+// the matrix cores.  With one rank every collective is the identity and the
+// path is the one-GPU blk_ge2band, launch for launch.
 // ==========================================================================
 namespace {
 struct DistBlk {
@@ -414,6 +420,13 @@ bool blk_dist_fits(int n, int P) {
 template <typename T>
 int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream_t s, int target, int *err) {
     const int P = C.nranks, me = C.rank;
+    if (P == 1) {
+        // one rank: every collective below is the identity and every rank-local
+        // piece is the whole panel -- the one-GPU blocked path is this path
+        // (its workspace is the head of this one's), launch for launch
+        BD_HIP(blk_ge2band<T>(A, m, n, lda, wsv, s, target, err));
+        return BRD_OK;
+    }
     const int n_loc = dist_local_cols(n, 32, P, me);
     const int kend = blk_columns(m, n, 32);
     char *ws = (char *)wsv;
@@ -451,11 +464,6 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         pa.gew = cw + 3072 * kCW;        // CqrWs::ew
         pa.gcnt = ctr + 64;
     };
-    // The X partials the next prep reads: all-reduced into ar (P > 1), or the
-    // read pass's split-K partials themselves (one rank: no sum, no copy)
-    const void *xpart = ar + 256 * 32, *xG = ar;
-    long xmp = 0;
-    int xks = 1;
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
             const int p = k0 / 32 + j, c = 32 * p, mr = m - c, mx = m - c - 32;
@@ -469,22 +477,20 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             // ---- X_{j-1} (every rank) + the column panel's QR (its owner) ----------
             const bool fold_qr = own && j > 0 && (foldm & 1);
             if (j > 0) {
-                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, xpart, xmp, xks, xG, tf + 1024 * (NBMAX + j - 1), sg0, lco);
+                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1), sg0,
+                                   lco);
                 if (fold_qr) gram_into(pa);
                 launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
-            // Q_t and the zero flag: broadcast with V' (P > 1), else where k_cqr_v left them
-            const double *qtp = P > 1 ? qt : cws + cqr_ws_qt(), *zp = P > 1 ? qt + 1024 : cws + cqr_ws_zero();
-            const FinArgs fq{qtp, zp, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
+            const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
             if (own) {
                 const T *src = j == 0 ? A + (size_t)c * lda + lco : (const T *)(ws + Ly.qp);
                 const long si = j == 0 ? lda : 1, st = j == 0 ? 1 : Ly.mp;
-                BD_HIP(launch_cqr<T>(src, si, st, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, P > 1 ? bc : nullptr, 32,
-                                     1, Tj, A + (size_t)c * lda + lco, lda, 1, ws, Ly, err, s, false, fq, 1,
-                                     P > 1 ? qt : nullptr, fold_qr));
+                BD_HIP(launch_cqr<T>(src, si, st, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, bc, 32, 1, Tj,
+                                     A + (size_t)c * lda + lco, lda, 1, ws, Ly, err, s, false, fq, 1, qt, fold_qr));
             }
-            if (P > 1) {
+            {
                 BD_TRY(C.bcast(bc, (size_t)mr * 32 * sizeof(T) + 1025 * sizeof(double), o, s));
                 if (!own) launch_dist_unpack_v<T>(bc, Lw + (size_t)c * 256 + 32 * j, mr, s);
             }
@@ -494,20 +500,12 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                                    Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
                                    Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j));
             // ---- the row panel: corrected locally, factored by a sharded CholeskyQR --
-            const bool fold_lq = P == 1 && (foldm & 2);
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
-                if (fold_lq) gram_into(pa);
                 launch_k_prep<T>(true, prep_grid(pa, api_device_cus()), pa, s);
                 BD_HIP(hipGetLastError());
             }
-            if (P == 1) {   // one rank: the whole row panel is here (no records, no middle pass)
-                const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj, A + (size_t)c * lda + lcs, 1,
-                                 lda};
-                BD_HIP(launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, nc, RwT + (size_t)(128 + 32 * j) * ldr + lcs, 1,
-                                     ldr, Ub + (size_t)lcs * 32, 32, 1, Sj, A + (size_t)c * lda + lcs, 1, lda, ws, Ly,
-                                     err, s, true, fl, 1, nullptr, fold_lq));
-            } else {
+            {
                 CqrArgs a;
                 a.src = ws + Ly.qp; a.si = 1; a.st = Ly.mp; a.M = std::max(nc, 0);
                 a.vdst = RwT + (size_t)(128 + 32 * j) * ldr + lcs; a.vsi = 1; a.vst = ldr;
@@ -527,16 +525,15 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                                  own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
                 const size_t rb = (size_t)kCqrRec * sizeof(double);
                 launch_k_cqr<T>(kCqrGram, nwg, a, fl, s);   // -> record bank 0: this rank's G1, exponent
-                if (P > 1) BD_TRY(C.allgather(rec + (size_t)me * kCqrRec, rec, rb, s));
+                BD_TRY(C.allgather(rec + (size_t)me * kCqrRec, rec, rb, s));
                 launch_k_cqr<T>(kCqrQ1, nwg, a, fl, s);     // R1 (every rank, the same), Q1 rows -> bank 1
-                if (P > 1) BD_TRY(C.allgather(rec + (size_t)(P + me) * kCqrRec, rec + (size_t)P * kCqrRec, rb, s));
+                BD_TRY(C.allgather(rec + (size_t)(P + me) * kCqrRec, rec + (size_t)P * kCqrRec, rb, s));
                 launch_k_cqr<T>(kCqrMid, nwg, a, fl, s);    // sCQR3's middle pass (shifted panels) -> bank 2
-                if (P > 1)
-                    BD_TRY(C.allgather(rec + (size_t)(2 * P + me) * kCqrRec, rec + (size_t)2 * P * kCqrRec, rb, s));
+                BD_TRY(C.allgather(rec + (size_t)(2 * P + me) * kCqrRec, rec + (size_t)2 * P * kCqrRec, rb, s));
                 // V rows into RwT and Ub; the top block's owner finishes inline (LU, S_j, the band block)
                 launch_k_cqr<T>(own2 ? kCqrVInline : kCqrV, nwg, a, fl, s);
                 BD_HIP(hipGetLastError());
-                if (P > 1) BD_TRY(C.bcast(Sj, 1024 * sizeof(T), o2, s));
+                BD_TRY(C.bcast(Sj, 1024 * sizeof(T), o2, s));
             }
             // ---- X pass (local columns), partials summed and all-reduced ------------
             if (nc > 0) {
@@ -544,21 +541,16 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                 BD_HIP(launch_rpass<T>(false, A + (size_t)(c + 32) * lda + lcs, lda, nc, mx, Ub + lcs * 32, 32,
                                        RwT + lcs, ldr, ws, Ly, ctr + 16, err, s, target, &ks_x, nullptr, nullptr, 0,
                                        nullptr, ar));
-                if (P > 1) {
-                    launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
-                } else {
-                    xpart = ws + Ly.part; xmp = Ly.mp; xks = ks_x;
-                }
+                launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
             } else {
                 BD_HIP(hipMemsetAsync(ar, 0, ((size_t)mx * 32 + 256 * 32) * sizeof(T), s));
-                xpart = ar + 256 * 32; xmp = 0; xks = 1;
             }
-            if (P > 1) BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32, dt, s));
+            BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32, dt, s));
         }
         // ---- block end: X_3 (every rank), the rank-256 update of my columns ---------
         const int k1 = k0 + NBMAX * 32;
         {
-            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, xpart, xmp, xks, xG, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
+            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
             launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
             BD_HIP(hipGetLastError());
         }

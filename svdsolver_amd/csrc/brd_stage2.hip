@@ -1207,6 +1207,10 @@ constexpr bool kS2Lag2 = BRD_S2_LAG2 != 0;
 #ifndef BRD_S2_DEFER_LAG2
 #define BRD_S2_DEFER_LAG2 1           // 0: deferred windows still wait for lag 3 (A/B of the fixup alone)
 #endif
+#ifndef BRD_S2_REGLOAD
+#define BRD_S2_REGLOAD 1              // 0: LDS-DMA only (A/B: N = 8192 fp64 72.9 vs 72.8 ms, fp32 62.9 vs 61.0)
+#endif
+template <typename T> constexpr int kRG = 16;   // loader: rows loaded into registers ahead of a full ring
 struct SweepFlags {
     int prog[12];    // tasks completed per compute wave
     int front[12];   // top row of each compute wave's next window (n when done)
@@ -1365,12 +1369,21 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 }
             }
         } else if (wave == S) {
-            // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
-            // (the k_band2bd_bundle loader: one global_load_lds_dwordx4 per
-            // interior row, up to kFly rows in flight, published oldest first in
-            // chunks of kChunk behind counted vmcnt waits; edge rows through
-            // registers)
+            // ---------------- loader wave: HBM -> ring ----------------
+            // Rows whose ring slots are free go in by LDS-DMA (one
+            // global_load_lds_dwordx4 per interior row, up to kFly rows in
+            // flight, published oldest first in chunks of kChunk behind counted
+            // vmcnt waits).  When the ring is full (the writers have not freed
+            // the next row's slot) and the previous bundle has already written
+            // rows back, the next kRG of them are loaded into registers ahead of
+            // their slots and stored into the ring (one 16-byte LDS store per
+            // lane) the moment each slot is freed: the ring recycle loop -- the
+            // trail releases a row, a writer frees its slot, the loader fills it
+            // -- is what paces a bundle (the ring was full before 98 % of the
+            // DMA issues), and this takes the HBM latency out of it.  Edge rows
+            // through registers.
             const int row_q = P * (int)sizeof(T) / 16;
+            const bool ql = lane < row_q;
             const unsigned row_bytes = (unsigned)(P * (int)sizeof(T));
             const unsigned ring_lds = (unsigned)(uintptr_t)ring;
             const unsigned ring_end = ring_lds + (unsigned)R * row_bytes;
@@ -1422,6 +1435,47 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                     wait_vmcnt(keep);
                     rl = ra - keep;
                     if (lane == 0) lds_st(&F->loaded, rl);
+                    TRP(beta, 0, rl);
+                    spins = 0;
+                } else if (BRD_S2_REGLOAD && !moved && ra < av && fr + R <= ra && ra >= 1 && ra <= dma_hi) {
+                    // the ring is full and rows are waiting upstream: the next
+                    // rows into registers, then into their slots as they free
+                    const int k = __builtin_amdgcn_readfirstlane(min(min(kRG<T>, av - ra), dma_hi + 1 - ra));
+                    u32x4 g[kRG<T>];
+                    {
+                        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                            (void *)(A + (long)ra * lda + ra - (b - 1)), (short)0, 0x7fffffff, 0x00020000);
+                        const int vo = 16 * (ql ? lane : 0);
+#pragma unroll
+                        for (int kk = 0; kk < kRG<T>; ++kk)   // (past k: row ra again, a fixed count)
+                            g[kk] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (unsigned)((kk < k ? kk : 0) * rstep), 16);
+                    }
+                    const int sl0 = (int)((dst - ring_lds) / row_bytes);
+                    int fl = fr + R;   // rows < fl have free slots
+#pragma unroll
+                    for (int kk = 0; kk < kRG<T>; ++kk) {
+                        if (kk < k) {
+                            const int r = ra + kk;
+                            if (r >= fl) {
+                                if (kk > 0 && lane == 0) lds_st(&F->loaded, r);
+                                int f2 = __builtin_amdgcn_readfirstlane(lds_ld(&F->freed));
+                                while (f2 + R <= r) {
+                                    __builtin_amdgcn_s_sleep(0);
+                                    if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 14); break; }
+                                    f2 = __builtin_amdgcn_readfirstlane(lds_ld(&F->freed));
+                                }
+                                fl = f2 + R;
+                            }
+                            const int sl = sl0 + kk >= R ? sl0 + kk - R : sl0 + kk;
+                            if (ql) *((u32x4 *)(ring + sl * P) + lane) = g[kk];
+                        }
+                    }
+                    ra += k;
+                    rl = ra;
+                    src += (long)k * rstep;
+                    dst += (unsigned)k * row_bytes;
+                    if (dst >= ring_end) dst -= ring_end - ring_lds;
+                    if (lane == 0) lds_st(&F->loaded, rl);   // LDS in order: after the rows
                     TRP(beta, 0, rl);
                     spins = 0;
                 } else if (!moved) {

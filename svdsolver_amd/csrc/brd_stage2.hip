@@ -1198,6 +1198,12 @@ namespace brd {
 //  * a compact role split (no SGPR spills: one window code path per kind).
 // ==========================================================================
 constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
+#ifndef BRD_S2_SWEEP_ROWS
+#define BRD_S2_SWEEP_ROWS 16   // rows per writer batch (same box, N = 8192: 8 / 16 / 24 / 32 rows
+                               // 102.6 / 73.7 / 77.3 / 72.8-73.2 ms fp64 -- 16: 71.5 beside 72.8 --,
+                               // 78.9 / 60.1 / 62.2 / 60.8 fp32)
+#endif
+constexpr int kSweepRows = BRD_S2_SWEEP_ROWS;
 #ifndef BRD_S2_LAG2
 #define BRD_S2_LAG2 0                 // 1: lag 2 with the deferred corner (A/B; bitwise the same band,
                                       // measured 93 ms against lag 3's 72 ms at N = 8192 fp64: the
@@ -1506,7 +1512,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
             }
         } else if (wave > S && wave <= S + kSweepWriters) {
             // ---------------- writer waves: ring -> HBM ----------------
-            // Batches of at most kWriteRows rows below all fronts (no sweep of
+            // Batches of at most kSweepRows rows below all fronts (no sweep of
             // the bundle touches them again), dealt alternately to the writer
             // waves so that one batch's drain overlaps the next batch's stores
             // (a single writer that drains each batch before taking the next
@@ -1533,7 +1539,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 for (;;) {
                     int fmin = n;
                     for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_ld(&F->front[s]));
-                    wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_ld(&F->loaded)), wb + kWriteRows));
+                    wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_ld(&F->loaded)), wb + kSweepRows));
                     if (wt > wb) break;
                     __builtin_amdgcn_s_sleep(0);
                     if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
@@ -1551,7 +1557,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 // interior half that does not wrap the ring is straight-line code
                 // (immediate LDS offsets, buffer stores with the row offset in
                 // soffset); anything else goes row by row.
-                constexpr int kH = kWriteRows / 2;
+                constexpr int kH = kSweepRows / 2;
                 const int sl0 = rg.slot(wb);
                 const unsigned rstride = (unsigned)gstep;
                 for (int r0 = 0; r0 < k; r0 += kH) {

@@ -284,3 +284,60 @@ def test_distributed_stage1_streams_with_own_communicators(world, mode, lanes, t
         ref = S.brd_p1(A, b)
         assert _band_err(bands[k], ref, b) <= 1e-12, k
         assert np.all(bands[k][~_band_mask(n, b)] == 0)
+
+
+def _edge_matrix(kind, n, b):
+    rng = np.random.default_rng(17)
+    if kind == "rank1_exact":
+        return np.outer(rng.standard_normal(n), rng.standard_normal(n))
+    if kind == "rank20_exact":
+        return rng.standard_normal((n, 20)) @ rng.standard_normal((20, n))
+    A = rng.uniform(1, 5, (n, n))
+    if kind == "dup_rows":      # the row panels' (LQ side) duplicated columns
+        A[9] = A[2]
+        A[100] = A[60]
+    elif kind == "zero_col_in_panel":
+        A[:, 5] = 0.0
+        A[:, 200] = 0.0
+    return A
+
+
+def _edge_worker(rank, world, port, n, b, kind, out_path):
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
+    import torch.distributed as tdist
+    from svdsolver_amd import dist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_host()
+    A = _edge_matrix(kind, n, b)
+    loc = torch.from_numpy(dist.shard(A, b, world, rank)).cuda()
+    dist.ge2band(loc, n, b)
+    B = dist.gather_band(loc, n, b, root=0)
+    if rank == 0:
+        np.save(out_path, B.cpu().numpy())
+    dist.finalize()
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["rank1_exact", "rank20_exact", "dup_rows", "zero_col_in_panel"])
+def test_distributed_structured_panels(world, kind, tmp_path):
+    """Exactly rank-deficient row panels on the sharded CholeskyQR (ADVICE r4:
+    the completion vectors of sCQR3's middle pass, k_cqr_mid, must keep the
+    transform orthogonal when the panel's rows are spread over ranks): the
+    gathered band keeps exact zeros outside it and the input's singular
+    values (fp64, 1e-12 sigma_max), as on one GPU (test_gpu_edges.py)."""
+    import torch.multiprocessing as mp
+    n, b = 512, 32
+    out = str(tmp_path / "band.npy")
+    mp.spawn(_edge_worker, args=(world, _free_port(), n, b, kind, out), nprocs=world, join=True)
+    band = np.load(out)
+    A = _edge_matrix(kind, n, b)
+    ref = np.linalg.svd(A, compute_uv=False)
+    assert np.all(np.isfinite(band))
+    assert np.all(band[~_band_mask(n, b)] == 0)
+    sb = np.linalg.svd(band, compute_uv=False)
+    assert np.max(np.abs(sb - ref)) <= 1e-12 * ref[0], np.max(np.abs(sb - ref)) / ref[0]

@@ -54,6 +54,7 @@ struct S2Fix {
     T alpha;   // the deferring window's reflector: w_j = alpha x_j (j >= 1), w_0 = 1
     T tau;
     T x31;     // x_31 (the corner's factor)
+    T xl;      // per lane l < 32: x_l of the deferring window (read with its source vector)
 };
 
 __device__ __forceinline__ double s2_readlane(double v, int l) {
@@ -71,22 +72,41 @@ __device__ __forceinline__ float s2_readlane(float v, int l) {
 //   tau = -s u1 / |x|, dot = a0 + alpha sigma, a0 -= tau dot,
 //   a_j -= tau dot alpha x_j.
 // Returns sigma' (and the scalars in f) for a deferred lane.
+// The two halves of the reflector: the partial sums over j = 0 .. 30 (they
+// start as the loads land), then -- after a deferred lane's fixup has
+// completed element 31 -- the rest.
+template <typename T>
+struct S2Sums {
+    T q0, q1, q2, q3, g0, g1, g2, g3;
+};
+// the sums materialised here, in program order: the compiler would otherwise
+// sink them below a fixup branch and wait for every load before the first FMA
+// (fp32 only: N = 8192 stage 2 60.0 -> 58.0 ms; fp64 measured 73.7 -> 74.2, so
+// fp64 leaves the schedule to the compiler)
+template <typename T>
+__device__ __forceinline__ void s2_pin(S2Sums<T> &u) {
+    if constexpr (sizeof(T) == 4)
+        asm volatile("" : "+v"(u.q0), "+v"(u.q1), "+v"(u.q2), "+v"(u.q3), "+v"(u.g0), "+v"(u.g1), "+v"(u.g2), "+v"(u.g3));
+}
 template <typename T, int N>
-__device__ __forceinline__ T s2_refl(T (&a)[N], const T (&x)[N], S2Fix<T> &f) {
+__device__ __forceinline__ S2Sums<T> s2_sums(const T (&a)[N], const T (&x)[N]) {
     static_assert(N == 32, "b = 32 windows");
-    T q0 = x[0] * x[0], q1 = (T)0, q2 = (T)0, q3 = (T)0;
-    T g0 = (T)0, g1 = (T)0, g2 = (T)0, g3 = (T)0;
+    S2Sums<T> u{x[0] * x[0], (T)0, (T)0, (T)0, (T)0, (T)0, (T)0, (T)0};
 #pragma unroll
     for (int j = 1; j < N - 1; j += 4) {
-        q1 = fma(x[j], x[j], q1);
-        g1 = fma(a[j], x[j], g1);
-        if (j + 1 < N - 1) { q2 = fma(x[j + 1], x[j + 1], q2); g2 = fma(a[j + 1], x[j + 1], g2); }
-        if (j + 2 < N - 1) { q3 = fma(x[j + 2], x[j + 2], q3); g3 = fma(a[j + 2], x[j + 2], g3); }
-        if (j + 3 < N - 1) { q0 = fma(x[j + 3], x[j + 3], q0); g0 = fma(a[j + 3], x[j + 3], g0); }
+        u.q1 = fma(x[j], x[j], u.q1);
+        u.g1 = fma(a[j], x[j], u.g1);
+        if (j + 1 < N - 1) { u.q2 = fma(x[j + 1], x[j + 1], u.q2); u.g2 = fma(a[j + 1], x[j + 1], u.g2); }
+        if (j + 2 < N - 1) { u.q3 = fma(x[j + 2], x[j + 2], u.q3); u.g3 = fma(a[j + 2], x[j + 2], u.g3); }
+        if (j + 3 < N - 1) { u.q0 = fma(x[j + 3], x[j + 3], u.q0); u.g0 = fma(a[j + 3], x[j + 3], u.g0); }
     }
-    q0 = fma(x[N - 1], x[N - 1], q0);
-    const T qq = (q0 + q1) + (q2 + q3);
-    const T sigp = (g0 + g1) + (g2 + g3);
+    return u;
+}
+template <typename T, int N>
+__device__ __forceinline__ T s2_apply(T (&a)[N], const T (&x)[N], S2Sums<T> u, S2Fix<T> &f) {
+    u.q0 = fma(x[N - 1], x[N - 1], u.q0);
+    const T qq = (u.q0 + u.q1) + (u.q2 + u.q3);
+    const T sigp = (u.g0 + u.g1) + (u.g2 + u.g3);
     const T sig = fma(a[N - 1], x[N - 1], sigp);
     const T rn = rsq_nr(qq);
     const T nrm = qq * rn;
@@ -107,20 +127,24 @@ __device__ __forceinline__ T s2_refl(T (&a)[N], const T (&x)[N], S2Fix<T> &f) {
     f.x31 = x[N - 1];
     return sigp;
 }
+template <typename T, int N>
+__device__ __forceinline__ T s2_refl(T (&a)[N], const T (&x)[N], S2Fix<T> &f) {
+    return s2_apply<T, N>(a, x, s2_sums<T, N>(a, x), f);
+}
 
 // Complete the previous window's deferred vector: element 31 of lanes 0..31
 // (lane 0: its pivot, lane 31: the corner, now final).  The pivot is this
 // window's x[31] as loaded and the corner comes from its own broadcast load,
 // so the reflector scalars and x[31]'s new value (the pivot's) need no
-// cross-lane reads of the window's data; xs: the deferring window's source
-// vector (LDS, 32 elements).
+// cross-lane reads of the window's data; f.xl: lane l's element of the
+// deferring window's source vector (registers, no LDS round trip).
 template <typename T, int N>
-__device__ __forceinline__ void s2_fixup(T (&a)[N], T (&x)[N], const S2Fix<T> &f, const T *xs, T corner, int lane) {
+__device__ __forceinline__ void s2_fixup(T (&a)[N], T (&x)[N], const S2Fix<T> &f, T corner, int lane) {
     const T a0 = x[N - 1];
     const T dot = fma(f.alpha, fma(corner, f.x31, f.sig), a0);
     const T tda = (f.tau * dot) * f.alpha;
     const T p = fma(-f.tau, dot, a0);   // the pivot's new value (lane 0's element 31)
-    if (lane < 32) a[N - 1] = lane == 0 ? p : fma(-tda, xs[lane], a[N - 1]);
+    if (lane < 32) a[N - 1] = lane == 0 ? p : fma(-tda, f.xl, a[N - 1]);
     x[N - 1] = p;
 }
 
@@ -141,13 +165,150 @@ struct S2Pub {
     }
 };
 
+// The fixup on element 31 alone (s2_fixup's arithmetic): a31 = this lane's
+// element 31, x31 = the source's, before the bulk of the window -- so the
+// previous window's completion is published as early as the window allows.
+template <typename T>
+__device__ __forceinline__ void s2_fixup1(T &a31, T &x31, const S2Fix<T> &f, T corner, int lane) {
+    const T dot = fma(f.alpha, fma(corner, f.x31, f.sig), x31);
+    const T tda = (f.tau * dot) * f.alpha;
+    const T p = fma(-f.tau, dot, x31);
+    if (lane < 32) a31 = lane == 0 ? p : fma(-tda, f.xl, a31);
+    x31 = p;
+}
+
+#ifndef BRD_S2_E31FIRST
+#define BRD_S2_E31FIRST 0   // 1: element 31 loaded and fixed before the window's bulk (A/B)
+#endif
+#if BRD_S2_E31FIRST
+// Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
+// j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
+// reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
+// nc = 32 (no predicates).  Element 31 (the deferred column of a fixup) is
+// loaded first and fixed before the bulk is used.
+template <typename T, bool FULL, bool LAG2>
+__device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
+                                            bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
+                                            const S2Pub &pub) {
+    constexpr int N = 32;
+    const bool rok = FULL || lane < nr;
+    const T *px = rg.row(i1) + j1;
+    T *pa = rg.row(i1 + (rok ? lane : 0)) + j1;
+    const bool c31 = FULL || N - 1 < nc;
+    T x31 = c31 ? px[N - 1] : (T)0;
+    T a31 = (c31 && rok) ? pa[N - 1] : (T)0;
+    const T corner = LAG2 ? rg.row(i1 + 31)[j1 + 31] : (T)0;   // (loads without branches: see s2_pin)
+    if (LAG2) fo.xl = px[lane & 31];
+    T a[N], x[N];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        const bool cok = FULL || j < nc;
+        x[j] = cok ? px[j] : (T)0;
+        a[j] = (cok && rok) ? pa[j] : (T)0;
+    }
+    if (LAG2 && fix) {   // the deferred column j1 + 31 of rows i1 .. i1 + 31
+        s2_fixup1<T>(a31, x31, fi, corner, lane);
+        if (lane < 32) pa[N - 1] = a31;
+        pub.publish(lane);
+    }
+    x[N - 1] = x31;
+    a[N - 1] = a31;
+    S2Sums<T> u = s2_sums<T, N>(a, x);
+    s2_pin(u);
+    const T sigp = s2_apply<T, N>(a, x, u, fo);
+    if (LAG2 && defer) {
+        fo.sig = s2_readlane(sigp, 63);
+        if ((lane & 31) == 31) fo.xl = x[N - 1];   // (the fixup above may have changed it)
+    }
+    if (rok && !(LAG2 && defer && lane == 63)) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (FULL || j < nc) pa[j] = a[j];
+    }
+}
+
+// Left window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior 32 x 64 at
+// j1 = i1); the reflector comes from column j1.  Lane q holds column j1 + q.
+// Rows that do not wrap the ring sit P - 1 elements apart: one base address
+// and immediate offsets.
+template <typename T, bool FULL, bool LAG2>
+__device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
+                                           bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
+                                           const S2Pub &pub) {
+    constexpr int N = 32;
+    const bool cok = FULL || lane < nc;
+    const int q = cok ? lane : 0;
+    const int s0 = rg.slot(i1);
+    const bool r31 = FULL || N - 1 < nr;
+    T a[N], x[N];
+    if (LAG2) fo.xl = rg.row(i1 + (lane & 31))[j1];
+    auto finish = [&](T *e31, T corner, T x31, T a31, auto store) {
+        if (LAG2 && fix) {   // the deferred row i1 + 31 of columns j1 .. j1 + 31
+            s2_fixup1<T>(a31, x31, fi, corner, lane);
+            if (lane < 32) *e31 = a31;
+            pub.publish(lane);
+        }
+        x[N - 1] = x31;
+        a[N - 1] = a31;
+        S2Sums<T> u = s2_sums<T, N>(a, x);
+        s2_pin(u);
+        const T sigp = s2_apply<T, N>(a, x, u, fo);
+        if (LAG2 && defer) {
+            fo.sig = s2_readlane(sigp, 63);
+            if ((lane & 31) == 31) fo.xl = x[N - 1];
+        }
+        if (cok && !(LAG2 && defer && lane == 63)) store();
+    };
+    if (s0 + N <= rg.R) {
+        T *bx = rg.d + s0 * rg.P + 31 + (j1 - i1);   // element (i1 + j, j1) at bx[j (P - 1)]
+        T *b31 = bx + (N - 1) * (rg.P - 1);
+        const T x31 = r31 ? b31[0] : (T)0;
+        const T a31 = (r31 && cok) ? b31[q] : (T)0;
+        const T corner = LAG2 ? b31[31] : (T)0;
+#pragma unroll
+        for (int j = 0; j < N - 1; ++j) {
+            const bool rk = FULL || j < nr;
+            x[j] = rk ? bx[j * (rg.P - 1)] : (T)0;
+            a[j] = (rk && cok) ? bx[j * (rg.P - 1) + q] : (T)0;
+        }
+        finish(b31 + q, corner, x31, a31, [&]() {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (FULL || j < nr) bx[j * (rg.P - 1) + q] = a[j];
+        });
+    } else {
+        T *rows[N];
+        int s = s0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            rows[j] = rg.d + s * rg.P + 31 + (j1 - i1) - j;
+            s = s + 1 == rg.R ? 0 : s + 1;
+        }
+        const T x31 = r31 ? rows[N - 1][0] : (T)0;
+        const T a31 = (r31 && cok) ? rows[N - 1][q] : (T)0;
+        const T corner = LAG2 ? rows[N - 1][31] : (T)0;
+#pragma unroll
+        for (int j = 0; j < N - 1; ++j) {
+            const bool rk = FULL || j < nr;
+            x[j] = rk ? rows[j][0] : (T)0;
+            a[j] = (rk && cok) ? rows[j][q] : (T)0;
+        }
+        finish(rows[N - 1] + q, corner, x31, a31, [&]() {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (FULL || j < nr) rows[j][q] = a[j];
+        });
+    }
+}
+
+#else
 // Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
 // j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
 // reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
 // nc = 32 (no predicates).
-template <typename T, bool FULL>
+template <typename T, bool FULL, bool LAG2>
 __device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
-                                            bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo, T *xs,
+                                            bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
                                             const S2Pub &pub) {
     constexpr int N = 32;
     const bool rok = FULL || lane < nr;
@@ -160,20 +321,21 @@ __device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1,
         x[j] = cok ? px[j] : (T)0;
         a[j] = (cok && rok) ? pa[j] : (T)0;
     }
-    if (fix) {   // the deferred column j1 + 31 of rows i1 .. i1 + 31
-        s2_fixup<T, N>(a, x, fi, xs, rg.row(i1 + 31)[j1 + 31], lane);
+    if (LAG2) fo.xl = px[lane & 31];                  // (loads without branches: see s2_pin)
+    const T corner = LAG2 ? rg.row(i1 + 31)[j1 + 31] : (T)0;
+    S2Sums<T> u = s2_sums<T, N>(a, x);   // (elements 0 .. 30: the fixup does not touch them)
+    s2_pin(u);
+    if (LAG2 && fix) {   // the deferred column j1 + 31 of rows i1 .. i1 + 31
+        s2_fixup1<T>(a[N - 1], x[N - 1], fi, corner, lane);
         if (lane < 32) pa[N - 1] = a[N - 1];
         pub.publish(lane);
     }
-    const T sigp = s2_refl<T, N>(a, x, fo);
-    if (defer) {
+    const T sigp = s2_apply<T, N>(a, x, u, fo);
+    if (LAG2 && defer) {
         fo.sig = s2_readlane(sigp, 63);
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < N; ++j) xs[j] = x[j];
-        }
+        if ((lane & 31) == 31) fo.xl = x[N - 1];   // (the fixup above may have changed it)
     }
-    if (rok && !(defer && lane == 63)) {
+    if (rok && !(LAG2 && defer && lane == 63)) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
             if (FULL || j < nc) pa[j] = a[j];
@@ -184,15 +346,31 @@ __device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1,
 // j1 = i1); the reflector comes from column j1.  Lane q holds column j1 + q.
 // Rows that do not wrap the ring sit P - 1 elements apart: one base address
 // and immediate offsets.
-template <typename T, bool FULL>
+template <typename T, bool FULL, bool LAG2>
 __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
-                                           bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo, T *xs,
+                                           bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
                                            const S2Pub &pub) {
     constexpr int N = 32;
     const bool cok = FULL || lane < nc;
     const int q = cok ? lane : 0;
     const int s0 = rg.slot(i1);
     T a[N], x[N];
+    if (LAG2) fo.xl = rg.row(i1 + (lane & 31))[j1];
+    auto finish = [&](T *e31, T corner, auto store) {
+        S2Sums<T> u = s2_sums<T, N>(a, x);
+        s2_pin(u);
+        if (LAG2 && fix) {   // the deferred row i1 + 31 of columns j1 .. j1 + 31
+            s2_fixup1<T>(a[N - 1], x[N - 1], fi, corner, lane);
+            if (lane < 32) *e31 = a[N - 1];
+            pub.publish(lane);
+        }
+        const T sigp = s2_apply<T, N>(a, x, u, fo);
+        if (LAG2 && defer) {
+            fo.sig = s2_readlane(sigp, 63);
+            if ((lane & 31) == 31) fo.xl = x[N - 1];
+        }
+        if (cok && !(LAG2 && defer && lane == 63)) store();
+    };
     if (s0 + N <= rg.R) {
         T *bx = rg.d + s0 * rg.P + 31 + (j1 - i1);   // element (i1 + j, j1) at bx[j (P - 1)]
 #pragma unroll
@@ -201,24 +379,12 @@ __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, 
             x[j] = rk ? bx[j * (rg.P - 1)] : (T)0;
             a[j] = (rk && cok) ? bx[j * (rg.P - 1) + q] : (T)0;
         }
-        if (fix) {   // the deferred row i1 + 31 of columns j1 .. j1 + 31
-            s2_fixup<T, N>(a, x, fi, xs, bx[(N - 1) * (rg.P - 1) + 31], lane);
-            if (lane < 32) bx[(N - 1) * (rg.P - 1) + q] = a[N - 1];
-            pub.publish(lane);
-        }
-        const T sigp = s2_refl<T, N>(a, x, fo);
-        if (defer) {
-            fo.sig = s2_readlane(sigp, 63);
-            if (lane == 0) {
-#pragma unroll
-                for (int j = 0; j < N; ++j) xs[j] = x[j];
-            }
-        }
-        if (cok && !(defer && lane == 63)) {
+        T *b31 = bx + (N - 1) * (rg.P - 1);
+        finish(b31 + q, LAG2 ? b31[31] : (T)0, [&]() {
 #pragma unroll
             for (int j = 0; j < N; ++j)
                 if (FULL || j < nr) bx[j * (rg.P - 1) + q] = a[j];
-        }
+        });
     } else {
         T *rows[N];
         int s = s0;
@@ -230,26 +396,15 @@ __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, 
             x[j] = rk ? rows[j][0] : (T)0;
             a[j] = (rk && cok) ? rows[j][q] : (T)0;
         }
-        if (fix) {
-            s2_fixup<T, N>(a, x, fi, xs, rows[N - 1][31], lane);
-            if (lane < 32) rows[N - 1][q] = a[N - 1];
-            pub.publish(lane);
-        }
-        const T sigp = s2_refl<T, N>(a, x, fo);
-        if (defer) {
-            fo.sig = s2_readlane(sigp, 63);
-            if (lane == 0) {
-#pragma unroll
-                for (int j = 0; j < N; ++j) xs[j] = x[j];
-            }
-        }
-        if (cok && !(defer && lane == 63)) {
+        finish(rows[N - 1] + q, LAG2 ? rows[N - 1][31] : (T)0, [&]() {
 #pragma unroll
             for (int j = 0; j < N; ++j)
                 if (FULL || j < nr) rows[j][q] = a[j];
-        }
+        });
     }
 }
+
+#endif
 
 // ---- wave pair (W = 2) ------------------------------------------------------
 // The pair's waves meet on the source vector: wave 1 raises its flag once it

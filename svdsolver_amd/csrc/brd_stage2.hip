@@ -649,6 +649,23 @@ struct SweepIter {
         }
         return w;
     }
+    // Whether task t+1's window is at least k x k (the state after task t;
+    // the lag-2 deferral's condition: the next window hosts the fixup).
+    __device__ bool next_at_least(int t, int k) const {
+        if (t + 1 >= ntask) return false;
+        int nr, nc;
+        if (t == 0) {
+            nr = min(i + bs, m) - (i + 1);
+            nc = min(i + bs + bs - 1, n) - (i + 1);
+        } else if (((t + 1) & 1) == 0) {   // a right window from the running t_left
+            nr = min(tl.i2 + bs - 1, m) - tl.i1;
+            nc = tl.j2 - min(tl.j1 + bs - 1, n);
+        } else {                           // the left window is t_left itself
+            nr = tl.i2 - tl.i1;
+            nc = tl.j2 - tl.j1;
+        }
+        return nr >= k && nc >= k;
+    }
     // Top row of task t+1 given the state after task t (window tops are
     // non-decreasing along a sweep); m once the sweep is finished.
     __device__ int next_top(int t) const {
@@ -1286,7 +1303,6 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
     T *ring = (T *)smem;
     const size_t ring_bytes = ((size_t)R * P * sizeof(T) + 15) & ~(size_t)15;
     SweepFlags *F = (SweepFlags *)(smem + ring_bytes);
-    T *xsc = (T *)(smem + ring_bytes + ((sizeof(SweepFlags) + 15) & ~(size_t)15));   // S x 32: deferring windows' x
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const S2Ring<T> rg{ring, P, R, magic};
     const int nbundles = (n - 1 + S - 1) / S;
@@ -1322,8 +1338,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
             SweepIter it;
             it.init(n, n, b, i, sigma);
             const int prev_ntask = wave > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
-            T *xs = xsc + 32 * wave;
-            S2Fix<T> fx{(T)0, (T)0, (T)0, (T)0};
+            S2Fix<T> fx{(T)0, (T)0, (T)0, (T)0, (T)0};
             bool pend = false;
             for (int t = 0; t < it.ntask; ++t) {
                 bool right;
@@ -1331,13 +1346,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 const int nr = w.i2 - w.i1, nc = w.j2 - w.j1;
                 const bool live = nr > 0 && nc > 0;
                 const bool full = live && (right ? (nr == 2 * b && nc == b) : (nr == b && nc == 2 * b));
-                bool defer = false;
-                if (full && t + 1 < it.ntask && kS2Lag2) {
-                    SweepIter it2 = it;
-                    bool rn;
-                    const Win wn = it2.task(t + 1, rn);
-                    defer = wn.i2 - wn.i1 >= b && wn.j2 - wn.j1 >= b;
-                }
+                const bool defer = kS2Lag2 && full && it.next_at_least(t, b);
                 int spins = 0;
                 TRT(beta, wave, t, 0);
                 if (wave > 0) {
@@ -1358,20 +1367,22 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                     const S2Pub pub{&F->prog[wave], &F->front[wave], t, w.i1};
                     S2Fix<T> fo;
                     if (right) {
-                        if (full) s2_right_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
-                        else      s2_right_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
+                        if (full) s2_right_w1<T, true, kS2Lag2>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, pub);
+                        else      s2_right_w1<T, false, kS2Lag2>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, pub);
                     } else {
-                        if (full) s2_left_w1<T, true>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
-                        else      s2_left_w1<T, false>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, xs, pub);
+                        if (full) s2_left_w1<T, true, kS2Lag2>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, pub);
+                        else      s2_left_w1<T, false, kS2Lag2>(rg, w.i1, w.j1, nr, nc, lane, pend, fx, defer, fo, pub);
                     }
                     if (defer) fx = fo;
                     asm volatile("" ::: "memory");
                 }
                 pend = defer;
                 TRT(beta, wave, t, 3);
-                if (!defer && lane == 0) {   // LDS in order: the window's ring stores land first
+                if (lane == 0) {   // LDS in order: the window's ring stores land first
+                    // (a deferring window's front too: its deferred lane lies in
+                    // the next window's rows; its progress waits for the fixup)
                     lds_st(&F->front[wave], it.next_top(t));
-                    lds_st(&F->prog[wave], t + 1);
+                    if (!defer) lds_st(&F->prog[wave], t + 1);
                 }
             }
         } else if (wave == S) {
@@ -1720,8 +1731,8 @@ static bool bundle_plan(int n, int b, int &S, int &R) {
 constexpr int kSweepSlack = 40;
 template <typename T>
 static size_t sweeps_lds_bytes(int R, int S) {
-    return (((size_t)R * ring_pitch<T>(32) * sizeof(T) + 15) & ~(size_t)15) + ((sizeof(SweepFlags) + 15) & ~(size_t)15) +
-           (kS2Lag2 ? (size_t)S * 32 * sizeof(T) : 0);
+    (void)S;
+    return (((size_t)R * ring_pitch<T>(32) * sizeof(T) + 15) & ~(size_t)15) + ((sizeof(SweepFlags) + 15) & ~(size_t)15);
 }
 template <typename T>
 static bool sweeps_plan(int n, int &S, int &R) {

@@ -8,6 +8,8 @@
 //   mode 1: production single-wave full windows (win_*_full, W = 1)
 //   mode 2: the new single-wave windows (brd_s2win.h)
 //   mode 3: the new wave-pair windows (brd_s2win.h, W = 2)
+//   mode 4: mode 2 with the lag-2 deferred corner (every window but the last
+//           defers its last lane; the next window completes it)
 #include "../svdsolver_amd/csrc/brd_stage2.hip"
 #include "../svdsolver_amd/csrc/brd_s2win.h"
 
@@ -23,8 +25,8 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
     constexpr int B = 32;
     const int P = ring_pitch<T>(B);
     T *ring = (T *)smem;
-    int *prog = (int *)(smem + (size_t)R * P * sizeof(T));   // 16 words
-    int *xr = prog + 16;                                      // 16 words
+    int *prog = (int *)(smem + (size_t)R * P * sizeof(T));   // 16 words (+16: mode 4 fronts)
+    int *xr = prog + 32;                                      // 16 words, then mode 4's x scratch
     constexpr int W = (MODE == 0 || MODE == 3) ? 2 : 1;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
@@ -33,7 +35,7 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
         unsigned h = (unsigned)e * 2654435761u;
         ring[e] = (T)(1.0 + (double)(h >> 8) / 16777216.0);
     }
-    if (threadIdx.x < 32) prog[threadIdx.x] = 0;
+    if (threadIdx.x < 48) prog[threadIdx.x] = 0;
     __syncthreads();
     if (wave >= W * S) {
         // background LDS traffic: read + write 768-B rows (a loader / writer stand-in)
@@ -55,9 +57,12 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
     const int sw = wave / W, pw = wave - sw * W;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     const int ntask = 2 * npairs;
+    S2Fix<T> fx{(T)0, (T)0, (T)0, (T)0, (T)0};
+    bool pend = false;
     for (int t = 0; t < ntask; ++t) {
+        const bool defer = MODE == 4 && t + 1 < ntask;
         if (sw > 0) {
-            const int need = min(t + 4, ntask);
+            const int need = min(t + (defer ? 3 : 4), ntask);
             for (int spin = 0; spin < (1 << 22); ++spin) {
                 int m = __hip_atomic_load(prog + W * (sw - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (W == 2) m = min(m, __hip_atomic_load(prog + W * (sw - 1) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -90,8 +95,17 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
             S2Fix<T> fi{}, fo;
             const S2Pub pub{prog + 30, prog + 31, 0, 0};
             T *xs = (T *)(xr + 16);
-            if (right) s2_right_w1<T, true>(rg, i1, i1 + 32, 64, 32, lane, false, fi, false, fo, xs, pub);
-            else       s2_left_w1<T, true>(rg, i1, i1, 32, 64, lane, false, fi, false, fo, xs, pub);
+            if (right) s2_right_w1<T, true, false>(rg, i1, i1 + 32, 64, 32, lane, false, fi, false, fo, pub);
+            else       s2_left_w1<T, true, false>(rg, i1, i1, 32, 64, lane, false, fi, false, fo, pub);
+        } else if constexpr (MODE == 4) {
+            const S2Ring<T> rg{ring, P, R, magic};
+            S2Fix<T> fo;
+            const S2Pub pub{prog + wave, prog + 16 + wave, t, 0};
+            T *xs = (T *)(xr + 16) + 32 * sw;
+            if (right) s2_right_w1<T, true, true>(rg, i1, i1 + 32, 64, 32, lane, pend, fx, defer, fo, pub);
+            else       s2_left_w1<T, true, true>(rg, i1, i1, 32, 64, lane, pend, fx, defer, fo, pub);
+            if (defer) fx = fo;
+            pend = defer;
         } else {
             const S2Ring<T> rg{ring, P, R, magic};
             S2Pair pr{xr + W * sw, pw, t + 1};
@@ -99,7 +113,7 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
             else       s2_left_w2<T, true>(rg, i1, 32, 64, lane, pr);
         }
         asm volatile("" ::: "memory");
-        if (lane == 0) __hip_atomic_store(prog + wave, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!(MODE == 4 && defer) && lane == 0) __hip_atomic_store(prog + wave, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) out[wave] = t1 - t0;
@@ -112,9 +126,9 @@ __global__ void __launch_bounds__((MODE == 0 || MODE == 3) ? 1024 : 512) k_chain
 template <typename T, int MODE>
 static void run(int S, int npairs, int noise) {
     const int P = brd::ring_pitch<T>(32);
-    int R = (160 * 1024 - 256) / (P * (int)sizeof(T));
+    int R = (160 * 1024 - 512 - 64 * 12 * (int)sizeof(T)) / (P * (int)sizeof(T));
     if (R > 400) R = 400;
-    const size_t lds = (size_t)R * P * sizeof(T) + 256;
+    const size_t lds = (size_t)R * P * sizeof(T) + 256 + 64 * 12 * sizeof(T) + 256;
     constexpr int W = (MODE == 0 || MODE == 3) ? 2 : 1;
     unsigned long long *o;
     (void)hipMalloc(&o, 64 * 8);
@@ -141,11 +155,13 @@ int main(int argc, char **argv) {
             run<double, 1>(S, npairs, noise);
             run<double, 2>(S, npairs, noise);
             run<double, 3>(S, npairs, noise);
+            run<double, 4>(S, npairs, noise);
         }
     for (int S = 1; S <= 5; S += 2) {
         run<float, 0>(S, npairs, 0);
         run<float, 2>(S, npairs, 0);
         run<float, 3>(S, npairs, 0);
+        run<float, 4>(S, npairs, 0);
     }
     return 0;
 }

@@ -1215,12 +1215,17 @@ namespace brd {
 //  * a compact role split (no SGPR spills: one window code path per kind).
 // ==========================================================================
 constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
-#ifndef BRD_S2_SWEEP_ROWS
-#define BRD_S2_SWEEP_ROWS 16   // rows per writer batch (same box, N = 8192: 8 / 16 / 24 / 32 rows
-                               // 102.6 / 73.7 / 77.3 / 72.8-73.2 ms fp64 -- 16: 71.5 beside 72.8 --,
-                               // 78.9 / 60.1 / 62.2 / 60.8 fp32)
-#endif
-constexpr int kSweepRows = BRD_S2_SWEEP_ROWS;
+// Rows per writer batch, by size (k_sweeps' template argument WR).  Same box,
+// N = 8192: 8 / 16 / 24 / 32 rows 102.6 / 73.7 / 77.3 / 72.8-73.2 ms fp64 (16:
+// 71.5 beside 72.8 in another pair), 78.9 / 60.1 / 62.2 / 60.8 fp32; N = 16384
+// fp64: 16 rows 156.2, 32 rows 146.0.  Between the two sizes (not measured)
+// the switch is at the midpoint.  BRD_S2_SWEEP_ROWS=16 / 32 forces either.
+constexpr int kSweepRowsSplitN = 12288;
+static int sweep_rows_for(int n) {
+    static const char *e = getenv("BRD_S2_SWEEP_ROWS");
+    if (e && (atoi(e) == 16 || atoi(e) == 32)) return atoi(e);
+    return n <= kSweepRowsSplitN ? 16 : 32;
+}
 #ifndef BRD_S2_LAG2
 #define BRD_S2_LAG2 0                 // 1: lag 2 with the deferred corner (A/B; bitwise the same band,
                                       // measured 93 ms against lag 3's 72 ms at N = 8192 fp64: the
@@ -1293,7 +1298,7 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <typename T>
+template <typename T, int WR>
 __global__ void __launch_bounds__(sweeps_max_threads<T>())
 k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
 {
@@ -1523,7 +1528,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
             }
         } else if (wave > S && wave <= S + kSweepWriters) {
             // ---------------- writer waves: ring -> HBM ----------------
-            // Batches of at most kSweepRows rows below all fronts (no sweep of
+            // Batches of at most WR rows below all fronts (no sweep of
             // the bundle touches them again), dealt alternately to the writer
             // waves so that one batch's drain overlaps the next batch's stores
             // (a single writer that drains each batch before taking the next
@@ -1550,7 +1555,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 for (;;) {
                     int fmin = n;
                     for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_ld(&F->front[s]));
-                    wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_ld(&F->loaded)), wb + kSweepRows));
+                    wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_ld(&F->loaded)), wb + WR));
                     if (wt > wb) break;
                     __builtin_amdgcn_s_sleep(0);
                     if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 15); break; }
@@ -1568,7 +1573,7 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
                 // interior half that does not wrap the ring is straight-line code
                 // (immediate LDS offsets, buffer stores with the row offset in
                 // soffset); anything else goes row by row.
-                constexpr int kH = kSweepRows / 2;
+                constexpr int kH = WR / 2;
                 const int sl0 = rg.slot(wb);
                 const unsigned rstride = (unsigned)gstep;
                 for (int r0 = 0; r0 < k; r0 += kH) {
@@ -1782,14 +1787,16 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         const int nbundles = (n - 1 + S - 1) / S;
         const dim3 block(64 * (S + 2 + kSweepWriters));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
-        const void *fn = (const void *)k_sweeps<T>;
+        const bool w32 = sweep_rows_for(n) == 32;
+        const void *fn = w32 ? (const void *)k_sweeps<T, 32> : (const void *)k_sweeps<T, 16>;
         const size_t lds = sweeps_lds_bytes<T>(R, S);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         const int cap = coresident_limit(fn, (int)block.x, lds);
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
-        hipLaunchKernelGGL((k_sweeps<T>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
+        if (w32) hipLaunchKernelGGL((k_sweeps<T, 32>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
+        else     hipLaunchKernelGGL((k_sweeps<T, 16>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const int W = fast32 ? s2_waves_per_sweep() : 1;

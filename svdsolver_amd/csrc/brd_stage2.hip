@@ -1222,7 +1222,7 @@ constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
 // the switch is at the midpoint.  BRD_S2_SWEEP_ROWS=16 / 32 forces either.
 constexpr int kSweepRowsSplitN = 12288;
 static int sweep_rows_for(int n) {
-    static const char *e = getenv("BRD_S2_SWEEP_ROWS");
+    const char *e = getenv("BRD_S2_SWEEP_ROWS");   // (read per call: tests switch it)
     if (e && (atoi(e) == 16 || atoi(e) == 32)) return atoi(e);
     return n <= kSweepRowsSplitN ? 16 : 32;
 }

@@ -594,3 +594,23 @@ def test_reduce_many_stage2_bitwise_under_contention(S):
         got = S.reduce_many([A.clone() for A in As], b, sigma=sigma, lanes=4)
         for (d0, e0), (d1, e1) in zip(ref, got):
             assert torch.equal(d0, d1) and torch.equal(e0, e1)
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_stage2_writer_batch_sizes_bitwise(S, dt, monkeypatch):
+    """k_sweeps' writer batch size (16 rows up to N = 12288, 32 above,
+    brd_stage2.hip sweep_rows_for) changes only when rows are handed to the
+    next bundle, never the arithmetic: both sizes give the same bidiagonal
+    bit for bit (n = 2048, fast mode, compat geometry)."""
+    import torch
+    n, b = 2048, 32
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    A = torch.from_numpy(np.random.default_rng(41).uniform(0, 5, (n, n))).to(tdt).cuda()
+    S.ge2band(A, b)
+    out = []
+    for rows in ("16", "32"):
+        monkeypatch.setenv("BRD_S2_SWEEP_ROWS", rows)
+        W = A.clone()
+        d, e = S.band2bd(W, b)
+        out.append((d.clone(), e.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

@@ -91,9 +91,12 @@ int blk_columns(int m, int n, int b) {
 // stream, but the two forms round the K1 sums differently, and a matrix's
 // band would then depend on whether it ran in a stream: not kept.
 // BRD_PREP_SPLIT=0 / 1 forces either form for A/B runs.)
-// cus: the device's CUs, not the overlap-reduced apply target, so that the
-// split (and with it the rounding of the K1 sums) is the same whether or not
-// the call runs beside stage 2
+// cus: the CUs the stream may use (api_apply_target: fewer beside a stage-2
+// reservation).  Sizing the split on the device's CUs instead (round 5,
+// ADVICE r4) made the prep kernels' rounding independent of the overlap, but
+// the read passes' K split already depends on it, and the
+// 8-lane stream measured 24.07 against 24.26 TFLOP/s (N = 8192 fp64, same
+// box): so the target, as in round 4.
 static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
@@ -260,7 +263,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c; p.zfill = 0;
                 p.upatch = x_patch ? 1 : 0;
                 gram_into(p, fold_qr);
-                launch_k_prep<T>(false, prep_grid(p, api_device_cus()), p, s);
+                launch_k_prep<T>(false, prep_grid(p, api_apply_target()), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -285,7 +288,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c + 32; p.zfill = 0;
                 p.vpatch = yfold ? 1 : 0;
                 gram_into(p, fold_lq);
-                launch_k_prep<T>(true, prep_grid(p, api_device_cus()), p, s);
+                launch_k_prep<T>(true, prep_grid(p, api_apply_target()), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -317,7 +320,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
             p.cc = k1; p.zfill = 0;
-            launch_k_prep<T>(false, prep_grid(p, api_device_cus()), p, s);
+            launch_k_prep<T>(false, prep_grid(p, api_apply_target()), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -480,7 +483,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                 PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1), sg0,
                                    lco);
                 if (fold_qr) gram_into(pa);
-                launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
+                launch_k_prep<T>(false, prep_grid(pa, api_apply_target()), pa, s);
                 BD_HIP(hipGetLastError());
             }
             const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
@@ -502,7 +505,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             // ---- the row panel: corrected locally, factored by a sharded CholeskyQR --
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
-                launch_k_prep<T>(true, prep_grid(pa, api_device_cus()), pa, s);
+                launch_k_prep<T>(true, prep_grid(pa, api_apply_target()), pa, s);
                 BD_HIP(hipGetLastError());
             }
             {
@@ -551,7 +554,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         const int k1 = k0 + NBMAX * 32;
         {
             PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
-            launch_k_prep<T>(false, prep_grid(pa, api_device_cus()), pa, s);
+            launch_k_prep<T>(false, prep_grid(pa, api_apply_target()), pa, s);
             BD_HIP(hipGetLastError());
         }
         const long lck = (long)dist_panels_before(k1 / 32, P, me) * 32;

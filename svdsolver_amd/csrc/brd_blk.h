@@ -191,6 +191,19 @@ struct CqrLds {
     int flags;
     double q[4][64][33];     // per-wave staging of 64 rows (Gram, coalesced stores); per-wave Gram partials
 };
+// The LDS of k_cqr_gram / k_cqr_q1: only what they use, the Gram staged in
+// halves of 32 rows per wave (gram_wave) -- 61 KB against CqrLds' 139 KB, so
+// in a stream of reductions such a workgroup leaves room on its CU for a
+// k_blkupd_p workgroup (88 KB) instead of holding the whole CU.
+struct CqrLdsS {
+    double g[32][kSP];
+    double r1[32][kSP];
+    double r1w[32][kSP];
+    double scl[kCW];
+    int e_w;
+    int flags;
+    double q[4][32][33];
+};
 
 __device__ __forceinline__ double rdl(double v, int l) {   // lane l's value, wave-uniform
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),

@@ -34,30 +34,38 @@ namespace blk {
 // ==========================================================================
 // Gram partial of this wave's rows (one per lane) accumulated into gacc
 // (the three distinct 16 x 16 blocks of the symmetric 32 x 32)
-__device__ __forceinline__ void gram_wave(CqrLds &L, int w, int lane, const double (&x)[32], double (&gacc)[3][4]) {
+// (staged in two halves of 32 rows, k-steps 0-7 then 8-15: the same MFMA
+// chain as one 64-row staging, in half the LDS -- CqrLdsS)
+template <class LDS>
+__device__ __forceinline__ void gram_wave(LDS &L, int w, int lane, const double (&x)[32], double (&gacc)[3][4]) {
     typedef Mf<double>::v4 v4;
-#pragma unroll
-    for (int t = 0; t < 32; ++t) L.q[w][lane][t] = x[t];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int qq = lane >> 4, l15 = lane & 15;
     v4 a00 = {gacc[0][0], gacc[0][1], gacc[0][2], gacc[0][3]};
     v4 a01 = {gacc[1][0], gacc[1][1], gacc[1][2], gacc[1][3]};
     v4 a11 = {gacc[2][0], gacc[2][1], gacc[2][2], gacc[2][3]};
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int k = 4 * s + qq;
-        const double v0 = L.q[w][k][l15], v1 = L.q[w][k][16 + l15];
-        a00 = Mf<double>::mma(v0, v0, a00);
-        a01 = Mf<double>::mma(v0, v1, a01);
-        a11 = Mf<double>::mma(v1, v1, a11);
+    for (int h = 0; h < 2; ++h) {
+        if ((lane >> 5) == h) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) L.q[w][lane & 31][t] = x[t];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int s = 8 * h; s < 8 * h + 8; ++s) {
+            const int k = 4 * s + qq - 32 * h;
+            const double v0 = L.q[w][k][l15], v1 = L.q[w][k][16 + l15];
+            a00 = Mf<double>::mma(v0, v0, a00);
+            a01 = Mf<double>::mma(v0, v1, a01);
+            a11 = Mf<double>::mma(v1, v1, a11);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) { gacc[0][g] = a00[g]; gacc[1][g] = a01[g]; gacc[2][g] = a11[g]; }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Cholesky G = R^T R (R upper) by one wave, lane c holding column c in
@@ -189,7 +197,8 @@ __device__ __forceinline__ void umul_row(double (&x)[32], const double (&Ri)[32]
 #ifndef BRD_GRAM_BATCH
 #define BRD_GRAM_BATCH 8    // partials per batch of loads in flight (A/B knob, tools/variant_lib.sh)
 #endif
-__device__ __forceinline__ void gram_sum_all(CqrLds &L, const double *gp, const double *scl, int nwg, long gs = 1024) {
+template <class LDS>
+__device__ __forceinline__ void gram_sum_all(LDS &L, const double *gp, const double *scl, int nwg, long gs = 1024) {
     const int tid = threadIdx.x;
     constexpr int GB = BRD_GRAM_BATCH;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -244,7 +253,8 @@ __device__ __forceinline__ void cqr_load_row(const CqrArgs &a, int i, double (&x
 // the four waves' partials summed in fixed order
 // (coh: agent-scope stores, for the distributed form's last-arriver sum in
 // the same kernel, cqr_to_record)
-__device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32], double *dst, bool coh = false) {
+template <class LDS>
+__device__ __forceinline__ void cqr_gram_partial(LDS &L, const double (&x)[32], double *dst, bool coh = false) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double gacc[3][4] = {};
     gram_wave(L, w, lane, x, gacc);
@@ -270,7 +280,8 @@ __device__ __forceinline__ void cqr_gram_partial(CqrLds &L, const double (&x)[32
 
 // the panel's exponent e (INT_MIN: the panel is zero) and the partials' scale
 // factors 2^(2 (e_k - e)) into L.scl
-__device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg, bool ones, long es = 1) {
+template <class LDS>
+__device__ __forceinline__ int cqr_exponent(LDS &L, const double *ew, int nwg, bool ones, long es = 1) {
     const int tid = threadIdx.x;
     __shared__ int ewl[kCW];
     if (tid < kCW) ewl[tid] = tid < nwg ? (int)ew[(size_t)tid * es] : INT_MIN;
@@ -292,7 +303,8 @@ __device__ __forceinline__ int cqr_exponent(CqrLds &L, const double *ew, int nwg
 __device__ __forceinline__ double *cqr_bank(const CqrArgs &a, int bank) {
     return a.rec + (size_t)bank * a.nrec * kCqrRec;
 }
-__device__ void cqr_to_record(CqrLds &L, const CqrArgs &a, const double *gp, const double *ew, int bank) {
+template <class LDS>
+__device__ void cqr_to_record(LDS &L, const CqrArgs &a, const double *gp, const double *ew, int bank) {
     const int tid = threadIdx.x, nwg = gridDim.x;
     __shared__ int last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's partial stores have landed
@@ -344,7 +356,7 @@ __device__ __forceinline__ GramSrc cqr_gram_src(const CqrArgs &a, int bank, cons
 
 template <typename T>
 __global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
-    __shared__ CqrLds L;
+    __shared__ CqrLdsS L;
     const int tid = threadIdx.x, lane = tid & 63, wg = blockIdx.x;
     CqrWs W(a.ws);
     double x[32];
@@ -377,7 +389,7 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
 
 template <typename T>
 __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
-    __shared__ CqrLds L;
+    __shared__ CqrLdsS L;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x;
     CqrWs W(a.ws);
     if (tid == 0) L.flags = 0;

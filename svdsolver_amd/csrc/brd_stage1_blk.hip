@@ -85,12 +85,11 @@ int blk_columns(int m, int n, int b) {
 }
 
 // the prep kernels' grid: split K halves (kPI items per workgroup) while
-// that grid fits the CUs the stream may use (one workgroup per CU: LDS),
-// else 2 kPI items per workgroup, one K range per wave.  (Never splitting
-// beside other work -- brd_set_overlap -- measured 23.8 -> 24.1 TFLOP/s in the
-// stream, but the two forms round the K1 sums differently, and a matrix's
-// band would then depend on whether it ran in a stream: not kept.
-// BRD_PREP_SPLIT=0 / 1 forces either form for A/B runs.)
+// that grid fits the CUs the stream may use (one workgroup per CU: LDS) and
+// nothing runs beside it, else 2 kPI items per workgroup, one K range per
+// wave.  The two forms round the K1 sums differently, so a matrix's band
+// depends on whether it ran in a stream -- as the read passes' split already
+// does.  BRD_PREP_SPLIT=0 / 1 forces either form for A/B.
 // cus: the CUs the stream may use (api_apply_target: fewer beside a stage-2
 // reservation).  Sizing the split on the device's CUs instead (round 5,
 // ADVICE r4) made the prep kernels' rounding independent of the overlap, but
@@ -101,7 +100,11 @@ static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
     const int mode = getenv("BRD_PREP_SPLIT") ? atoi(getenv("BRD_PREP_SPLIT")) : -1;   // A/B: 0 never, 1 always
-    p.split = mode == 0 ? 0 : (mode == 1 || n1 <= cus) ? 1 : 0;
+    // beside other work (a stage-2 reservation: a stream of reductions) never
+    // split: half the workgroups, each holding a whole CU (LDS) for the same
+    // ~20 us, leave CUs to the other lanes' passes (8-lane stream, N = 8192
+    // fp64, same box: 24.36 / 24.39 -> 24.82 / 24.55 TFLOP/s)
+    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !api_overlap_active())) ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 

@@ -340,9 +340,11 @@ def test_cli_svd_runs(S):
 def test_reduce_many_pipelined_matches_serial(S, lanes):
     """reduce_many: stage 2 of matrix i on its own stream (32 workgroups) beside
     stage 1 of matrix i+1 (the remaining CUs).  Every matrix gets the serial
-    path's band bit for bit (the launch sizing under the overlap changes which
-    workgroup runs which slabs, never the per-element arithmetic order) and,
-    with the sigma geometry, the input's singular values to 1e-12 sigma_max."""
+    path's band up to rounding (beside a reservation the prep kernels do not
+    split K and the read passes split it over fewer CUs: fixed-order sums over
+    a different split; 1e-13 of the band's largest entry),
+    exact zeros outside it, and with the sigma geometry the input's singular
+    values to 1e-12 sigma_max."""
     import torch
     rng = np.random.default_rng(41)
     n, b, k = 1024, 32, 4
@@ -373,7 +375,7 @@ def test_reduce_many_pipelined_matches_serial(S, lanes):
         S.set_overlap(0)
     for M, ref_band in zip(mats, bands):
         B = np.abs(M.cpu().numpy())
-        assert np.array_equal(B, ref_band)
+        assert np.max(np.abs(B - ref_band)) <= 1e-13 * np.max(ref_band)
         assert np.all(B[~inb] == 0)
 
 
@@ -381,8 +383,10 @@ def test_stage1_f32_overlap_matches_serial(S):
     """fp32 stage 1 under a brd_set_overlap reservation runs the trailing update
     compiled for two workgroups per CU (LDS-staged slab, launch_apply's occ2),
     alone the register-resident variant: both issue the same MFMA chain on the
-    same operands, so the band is bit for bit the serial one (including the
-    upper-level applies' 8-slab floor, which only regroups slabs)."""
+    same operands (including the upper-level applies' 8-slab floor, which only
+    regroups slabs).  The blocked path's prep kernels do not split K beside a
+    reservation, so the band matches the serial one up to rounding (2e-6 of
+    its largest entry in fp32), with exact zeros outside it."""
     import torch
     rng = np.random.default_rng(47)
     n, b, k = 1024, 32, 3
@@ -406,7 +410,7 @@ def test_stage1_f32_overlap_matches_serial(S):
     inb = (j >= i) & (j - i <= b)
     for M, R in zip(mats, ref):
         B = M.cpu().numpy()
-        assert np.array_equal(B, R)
+        assert np.max(np.abs(np.abs(B) - np.abs(R))) <= 2e-6 * np.max(np.abs(R))
         assert np.all(B[~inb] == 0)
 
 
@@ -581,10 +585,16 @@ def test_reduce_many_stage2_bitwise_under_contention(S):
     n, b, k = 1536, 32, 8
     As = [torch.from_numpy(rng.uniform(0, 5, (n, n))).cuda() for _ in range(k)]
     bands = []
-    for A in As:
-        M = A.clone()
-        S.ge2band(M, b)
-        bands.append(M)
+    # stage 1 under the same reservation reduce_many sets (its launch sizing,
+    # hence its rounding, depends on it): the bands reduce_many's sweeps get
+    S.set_overlap(S.overlap_cus(n))
+    try:
+        for A in As:
+            M = A.clone()
+            S.ge2band(M, b)
+            bands.append(M)
+    finally:
+        S.set_overlap(0)
     for sigma in (False, True):
         ref = []
         for Bd in bands:

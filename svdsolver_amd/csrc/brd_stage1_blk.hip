@@ -118,8 +118,14 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     a.src = src; a.ld = ld; a.vsrc = vsrc; a.vld = vld; a.bsrc = bsrc; a.bld = bld;
     a.K = K; a.M = M;
     a.mtiles = (M + kMT - 1) / kMT;
-    static const int rpx = getenv("BRD_BLK_RPX") ? std::max(1, atoi(getenv("BRD_BLK_RPX"))) : 1;   // tuning
-    target *= rpx;
+    // Beside a stage-2 reservation (a stream of reductions) a pass is sized for
+    // half the CUs: the other lanes' kernels run on the rest (8-lane stream,
+    // N = 8192 fp64, same box: target x 1 / 0.75 / 0.5 / 0.375 / 0.25 ->
+    // 24.73-24.84 / 24.94 / 25.05-25.15 / 24.78 / 24.10-24.23 TFLOP/s).
+    // BRD_BLK_RPX scales the target further (A/B).
+    static const double rpx = getenv("BRD_BLK_RPX") ? std::max(0.125, atof(getenv("BRD_BLK_RPX"))) : 1.0;
+    if (api_overlap_active()) target = std::max(1, target / 2);
+    target = std::max(1, (int)(target * rpx));
     int ks, nwg;
     a.tiles = a.ns = a.wst = 0;
     if (rpass_dma_ok(yp, K, M, sizeof(T), src, ld, vsrc, vld, bsrc, bld) && K > 0) {

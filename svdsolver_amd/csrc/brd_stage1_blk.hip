@@ -96,6 +96,13 @@ int blk_columns(int m, int n, int b) {
 // the read passes' K split already depends on it, and the
 // 8-lane stream measured 24.07 against 24.26 TFLOP/s (N = 8192 fp64, same
 // box): so the target, as in round 4.
+// Beside a stage-2 reservation (a stream of reductions) at N <= 12288 the
+// prep kernels do not split K and the read passes are sized for half the
+// target (prep_grid, launch_rpass): at 8192 the 8-lane stream went 24.4 ->
+// 25.2 TFLOP/s; at 16384 the same sizing took it from 33.4 to 25.9 (30.3 with
+// the halving on passes <= 12288 wide only), so larger matrices keep the
+// one-at-a-time sizing.  Set per call by blk_ge2band / blk_ge2band_dist.
+static thread_local bool t_lean = false;
 static dim3 prep_grid(PrepArgs &p, int cus) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
@@ -104,7 +111,7 @@ static dim3 prep_grid(PrepArgs &p, int cus) {
     // split: half the workgroups, each holding a whole CU (LDS) for the same
     // ~20 us, leave CUs to the other lanes' passes (8-lane stream, N = 8192
     // fp64, same box: 24.36 / 24.39 -> 24.82 / 24.55 TFLOP/s)
-    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !api_overlap_active())) ? 1 : 0;
+    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !t_lean)) ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 
@@ -124,7 +131,7 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     // 24.73-24.84 / 24.94 / 25.05-25.15 / 24.78 / 24.10-24.23 TFLOP/s).
     // BRD_BLK_RPX scales the target further (A/B).
     static const double rpx = getenv("BRD_BLK_RPX") ? std::max(0.125, atof(getenv("BRD_BLK_RPX"))) : 1.0;
-    if (api_overlap_active()) target = std::max(1, target / 2);
+    if (t_lean) target = std::max(1, target / 2);
     target = std::max(1, (int)(target * rpx));
     int ks, nwg;
     a.tiles = a.ns = a.wst = 0;
@@ -210,6 +217,7 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
 // the caller finishes the remaining panels with the per-panel path.
 template <typename T>
 hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, int target, int *err) {
+    t_lean = api_overlap_active() && std::max(m, n) <= 12288;
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, n, sizeof(T));
     const int kend = blk_columns(m, n, 32);
@@ -441,6 +449,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
     }
     const int n_loc = dist_local_cols(n, 32, P, me);
     const int kend = blk_columns(m, n, 32);
+    t_lean = api_overlap_active() && std::max(m, n) <= 12288;
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, std::max(n_loc, 1), sizeof(T));
     const DistBlk D = dist_blk_layout(m, n, P, me, sizeof(T));

@@ -40,8 +40,8 @@ library's per-launch events (for the stage-1 apply stamped by the launch
 itself, hipExtLaunchKernel) for the dominant kernel's roofline object.  Also
 the CPU baseline: the reference's own tiled algorithm (built from its
 sources by oracle/Makefile) timed on this host at N = 320, 640, 1024 (about
-10-20 s), with a c N^3 + d N^2 fit extrapolated to the GPU problem size (labelled as
-such).
+10-20 s) and 2048, extrapolated cubically from the largest sample to the GPU
+problem size (labelled as such).
 """
 from __future__ import annotations
 
@@ -143,8 +143,9 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
     the reference's sources by oracle/Makefile (README.md:32 flags minus
     -march=native), on n x n fp64 matrices uniform in [0,5), b = band, at each
     n in `sizes`.  OpenMP threads = the job's CPU share (OMP_NUM_THREADS, else
-    the affinity set).  A least-squares c n^3 + d n^2 fit over the samples gives the
-    EXTRAPOLATED time at the GPU problem size (not measured: ~15 min at 8192).
+    the affinity set).  The EXTRAPOLATED time at the GPU problem size is cubic
+    from the largest sample (not measured: ~40 min at 8192); a least-squares
+    c n^3 + d n^2 fit over the samples is reported beside it.
     Falls back to the single-threaded C oracle (kind "port")."""
     import ctypes
     import numpy as np
@@ -180,7 +181,12 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
     M = np.array([[float(n) ** 3 / t, float(n) ** 2 / t] for n, t in pts])
     coef = np.linalg.lstsq(M, np.ones(len(pts)), rcond=None)[0] if len(pts) >= 2 else np.array([dt / n_s ** 3, 0.0])
     c, d = max(float(coef[0]), 0.0), max(float(coef[1]), 0.0)
-    t_ext = c * float(gpu_n) ** 3 + d * float(gpu_n) ** 2
+    t_fit = c * float(gpu_n) ** 3 + d * float(gpu_n) ** 2
+    # the reported extrapolation is CUBIC from the largest sample (VERDICT r5:
+    # the fit's n^2 term flatters the CPU 2.3x per flop at 8192; SURVEY.md
+    # section 6 measured the reference scaling cubically, 2048 -> 4096: 43.5 ->
+    # 338.5 s); the fit is kept beside it for reference
+    t_ext = dt * (float(gpu_n) / n_s) ** 3
     phys = hc.get("physical_cores")
     cores_note = (f"{used} OpenMP threads = the job's CPU share on this host (OMP_NUM_THREADS; the pool sizes "
                   f"a one-GPU job at 16 CPUs); the host has {phys} physical cores"
@@ -194,11 +200,11 @@ def cpu_baseline(sizes, band: int, gpu_n: int) -> dict:
             "sizes_s": {str(n): round(t, 3) for n, t in pts},
             "extrapolated": {"n": gpu_n, "seconds": round(t_ext, 1),
                              "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_ext / 1e9, 4),
-                             "basis": "least-squares c*n^3 + d*n^2 (relative error) over the sampled sizes "
-                                      + ",".join(str(n) for n, _ in pts) + "; NOT measured",
-                             "note": ("samples <= 1024 only: the LESS conservative fit (the default "
-                                      "--cpu-n 320,640,1024,2048 adds the 2048 sample, ~40 s)")
-                             if max(n for n, _ in pts) < 2048 else "2048-inclusive fit"}}
+                             "basis": f"cubic from the largest sample (t({n_s}) * ({gpu_n}/{n_s})^3); NOT measured",
+                             "fit_c_n3_d_n2": {"seconds": round(t_fit, 1),
+                                               "gflops": round(8.0 / 3.0 * gpu_n ** 3 / t_fit / 1e9, 4),
+                                               "basis": "least-squares over " + ",".join(str(n) for n, _ in pts)
+                                                        + " (less conservative: its n^2 term dominates at these sizes)"}}}
 
 
 def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):
@@ -515,8 +521,6 @@ def main():
         # sweep may still be running (the stage-1 stream also waits for that
         # sweep).
         nbuf = 2 if pipelined else 1
-        Bfull = [[torch.empty((n, n), dtype=tdt, device=dev) for _ in range(nbuf)] for _ in range(lanes)]
-        s2_done = [[None] * nbuf for _ in range(lanes)]
 
         def root_of(j):
             return j % world if pipelined else 0
@@ -524,20 +528,28 @@ def main():
         def band_of(j):
             return j % lanes, (j // lanes) % nbuf
 
+        # only the band buffers this rank roots, allocated before any timed
+        # region (with 8 lanes over 8 ranks: lane r's two buffers on rank r,
+        # 4 GB at N = 16384 instead of 32 GB; 8 host-callback ranks sharing
+        # one GPU would not fit otherwise)
+        Bfull = {key: torch.empty((n, n), dtype=tdt, device=dev)
+                 for key in sorted({band_of(j) for j in range(nmat) if root_of(j) == rank})}
+        s2_done = {key: None for key in Bfull}
+
         def stage1(A, j):
             D.ge2band(A, n, b, sync=False)
-            r, (ln, k) = root_of(j), band_of(j)
-            if rank == r and s2_done[ln][k] is not None:
-                torch.cuda.current_stream(dev).wait_event(s2_done[ln][k])
-            D.gather_band(A, n, b, root=r, out=Bfull[ln][k] if rank == r else None, sync=False)
+            r, key = root_of(j), band_of(j)
+            if rank == r and s2_done[key] is not None:
+                torch.cuda.current_stream(dev).wait_event(s2_done[key])
+            D.gather_band(A, n, b, root=r, out=Bfull[key] if rank == r else None, sync=False)
 
         def stage2(A, j):
             if rank == root_of(j):
-                ln, k = band_of(j)
-                S.band2bd(Bfull[ln][k], b, sigma=args.s2 == "sigma", sync=False, extract=False)
+                key = band_of(j)
+                S.band2bd(Bfull[key], b, sigma=args.s2 == "sigma", sync=False, extract=False)
                 e = torch.cuda.Event()
                 e.record(torch.cuda.current_stream(dev))
-                s2_done[ln][k] = e
+                s2_done[key] = e
     else:
         base = torch.rand((n, n), dtype=tdt, device=dev, generator=g) * 5.0
         mats = []

@@ -101,9 +101,23 @@ int blk_columns(int m, int n, int b) {
 // target (prep_grid, launch_rpass): at 8192 the 8-lane stream went 24.4 ->
 // 25.2 TFLOP/s; at 16384 the same sizing took it from 33.4 to 25.9 (30.3 with
 // the halving on passes <= 12288 wide only), so larger matrices keep the
-// one-at-a-time sizing.  Set per call by blk_ge2band / blk_ge2band_dist.
-static thread_local bool t_lean = false;
-static dim3 prep_grid(PrepArgs &p, int cus) {
+// one-at-a-time sizing.
+//
+// The sizing of one call's launches is fixed when the call starts and passed
+// to every launcher (no hidden per-thread state):
+//   target  workgroups a bandwidth launch may fill (api_apply_target: the
+//           device's CUs, less a stage-2 reservation);
+//   lean    beside a stage-2 reservation and max(m, n) <= kLeanMaxN: no prep
+//           K split, read passes sized for target / 2 (the measured rule above).
+static constexpr int kLeanMaxN = 12288;
+struct S1Launch {
+    int target;
+    bool lean;
+};
+static S1Launch s1_launch(int m, int n, int target) {
+    return S1Launch{target, api_overlap_active() && std::max(m, n) <= kLeanMaxN};
+}
+static dim3 prep_grid(PrepArgs &p, const S1Launch &lc) {
     const int items = std::max(p.items, p.zfill);
     const int n1 = (items + kPI - 1) / kPI;
     const int mode = getenv("BRD_PREP_SPLIT") ? atoi(getenv("BRD_PREP_SPLIT")) : -1;   // A/B: 0 never, 1 always
@@ -111,14 +125,14 @@ static dim3 prep_grid(PrepArgs &p, int cus) {
     // split: half the workgroups, each holding a whole CU (LDS) for the same
     // ~20 us, leave CUs to the other lanes' passes (8-lane stream, N = 8192
     // fp64, same box: 24.36 / 24.39 -> 24.82 / 24.55 TFLOP/s)
-    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= cus && !t_lean)) ? 1 : 0;
+    p.split = mode == 0 ? 0 : (mode == 1 || (n1 <= lc.target && !lc.lean)) ? 1 : 0;
     return dim3(std::max(1, p.split ? n1 : (items + 2 * kPI - 1) / (2 * kPI)));
 }
 
 template <typename T>
 static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, const T *bsrc, long bld, const T *vsrc,
                                long vld, char *ws, const BlkLayout &Ly, int *counter, int *err, hipStream_t s,
-                               int target, int *ksplit_out, const FinArgs *fin, T *pbase, long pstride,
+                               const S1Launch &lc, int *ksplit_out, const FinArgs *fin, T *pbase, long pstride,
                                const double *psgn, void *vout = nullptr, bool *vfolded = nullptr, int va = 0,
                                int vb = 0) {
     RpArgs a;
@@ -131,7 +145,7 @@ static hipError_t launch_rpass(bool yp, const T *src, long ld, int K, int M, con
     // 24.73-24.84 / 24.94 / 25.05-25.15 / 24.78 / 24.10-24.23 TFLOP/s).
     // BRD_BLK_RPX scales the target further (A/B).
     static const double rpx = getenv("BRD_BLK_RPX") ? std::max(0.125, atof(getenv("BRD_BLK_RPX"))) : 1.0;
-    if (t_lean) target = std::max(1, target / 2);
+    int target = lc.lean ? std::max(1, lc.target / 2) : lc.target;
     target = std::max(1, (int)(target * rpx));
     int ks, nwg;
     a.tiles = a.ns = a.wst = 0;
@@ -217,7 +231,7 @@ static hipError_t launch_cqr(const T *src, long si, long st, int M, T *vdst, lon
 // the caller finishes the remaining panels with the per-panel path.
 template <typename T>
 hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, int target, int *err) {
-    t_lean = api_overlap_active() && std::max(m, n) <= 12288;
+    const S1Launch lc = s1_launch(m, n, target);
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, n, sizeof(T));
     const int kend = blk_columns(m, n, 32);
@@ -280,7 +294,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c; p.zfill = 0;
                 p.upatch = x_patch ? 1 : 0;
                 gram_into(p, fold_qr);
-                launch_k_prep<T>(false, prep_grid(p, api_apply_target()), p, s);
+                launch_k_prep<T>(false, prep_grid(p, lc), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 e = launch_cqr<T>((const T *)(ws + Ly.qp), 1, Ly.mp, mr, Lw + (size_t)c * 256 + 32 * j, 256, 1, nullptr, 0, 0, Tj,
@@ -291,7 +305,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             int ks_y = 1;
             bool yfold = false;
             e = launch_rpass<T>(true, A + (size_t)c * lda + c + 32, lda, mr, n2, Lw + (size_t)c * 256 + 32 * j, 256,
-                                Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
+                                Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, lc, &ks_y, &fq,
                                 Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j, nullptr, &yfold, 32 * j, 32 * j);
             if (e != hipSuccess) return e;
             {
@@ -305,7 +319,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
                 p.cc = c + 32; p.zfill = 0;
                 p.vpatch = yfold ? 1 : 0;
                 gram_into(p, fold_lq);
-                launch_k_prep<T>(true, prep_grid(p, api_apply_target()), p, s);
+                launch_k_prep<T>(true, prep_grid(p, lc), p, s);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -319,7 +333,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             bool xfold = false;
             e = launch_rpass<T>(false, A + (size_t)(c + 32) * lda + c + 32, lda, n2, m - c - 32,
                                 Ub + (size_t)(c + 32) * 32, 32, RwT + c + 32, ldr, ws, Ly, ctr + 16, err, s,
-                                target, &ks_x, inl ? nullptr : &fl,
+                                lc, &ks_x, inl ? nullptr : &fl,
                                 inl ? nullptr : RwT + (size_t)(128 + 32 * j) * ldr + c + 32, ldr + 1, sgl + 32 * j,
                                 nullptr, &xfold, 32 * (j + 1), 32 * j);   // prep_qr(j + 1) / the block end read these
             x_patch = !inl && xfold;   // prep_qr of the next panel patches U_j's top block
@@ -337,7 +351,7 @@ hipError_t blk_ge2band(T *A, int m, int n, long lda, void *wsv, hipStream_t s, i
             p.c = k1; p.j = NBMAX; p.items = m - k1; p.reduce = 1; p.factor = 0;
             p.sgn = sg_prev;   // the block's last LQ panel finished inline: zeros
             p.cc = k1; p.zfill = 0;
-            launch_k_prep<T>(false, prep_grid(p, api_apply_target()), p, s);
+            launch_k_prep<T>(false, prep_grid(p, lc), p, s);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -449,7 +463,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
     }
     const int n_loc = dist_local_cols(n, 32, P, me);
     const int kend = blk_columns(m, n, 32);
-    t_lean = api_overlap_active() && std::max(m, n) <= 12288;
+    const S1Launch lc = s1_launch(m, n, target);
     char *ws = (char *)wsv;
     const BlkLayout Ly = blk_layout(m, std::max(n_loc, 1), sizeof(T));
     const DistBlk D = dist_blk_layout(m, n, P, me, sizeof(T));
@@ -460,7 +474,10 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
     T *bc = (T *)(ws + D.bc), *ar = (T *)(ws + D.ar);
     double *rec = (double *)(ws + D.rec);
     const int dt = sizeof(T) == 8 ? BRD_DT_F64 : BRD_DT_F32;
-    BD_HIP(hipMemsetAsync(ctr, 0, 64 * sizeof(int), s));
+    // every counter, the prep Gram groups' [64, 64 + kCW) included: the workspace
+    // is shared with the per-panel tail and the band gather, and a nonzero
+    // group counter would hold back the last-arriver's Gram sum
+    BD_HIP(hipMemsetAsync(ctr, 0, (64 + kCW) * sizeof(int), s));
     double *sgq = (double *)(ws + Ly.sg), *sgl = sgq + NBMAX * 32, *sg0 = sgq + 2 * NBMAX * 32;
     BD_HIP(hipMemsetAsync(sg0, 0, 32 * sizeof(double), s));
     const double *cws = (const double *)(ws + Ly.cws);
@@ -501,7 +518,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                 PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1), sg0,
                                    lco);
                 if (fold_qr) gram_into(pa);
-                launch_k_prep<T>(false, prep_grid(pa, api_apply_target()), pa, s);
+                launch_k_prep<T>(false, prep_grid(pa, lc), pa, s);
                 BD_HIP(hipGetLastError());
             }
             const FinArgs fq{qt, qt + 1024, sgq + 32 * j, Tj, own ? (void *)(A + (size_t)c * lda + lco) : nullptr, lda, 1};
@@ -518,12 +535,12 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             // ---- Y pass (local columns; every rank finishes the QR panel) -----------
             int ks_y = 1;
             BD_HIP(launch_rpass<T>(true, A + (size_t)c * lda + lcs, lda, mr, nc, Lw + (size_t)c * 256 + 32 * j, 256,
-                                   Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, target, &ks_y, &fq,
+                                   Lw + (size_t)c * 256, 256, ws, Ly, ctr + 16, err, s, lc, &ks_y, &fq,
                                    Lw + (size_t)c * 256 + 32 * j, 257, sgq + 32 * j));
             // ---- the row panel: corrected locally, factored by a sharded CholeskyQR --
             {
                 PrepArgs pa = prep(c, j, nc, 0, 0, ws + Ly.part, Ly.mp, ks_y, ws + Ly.vout, Tj, sgq + 32 * j, lcs);
-                launch_k_prep<T>(true, prep_grid(pa, api_apply_target()), pa, s);
+                launch_k_prep<T>(true, prep_grid(pa, lc), pa, s);
                 BD_HIP(hipGetLastError());
             }
             {
@@ -560,7 +577,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             if (nc > 0) {
                 int ks_x = 1;
                 BD_HIP(launch_rpass<T>(false, A + (size_t)(c + 32) * lda + lcs, lda, nc, mx, Ub + lcs * 32, 32,
-                                       RwT + lcs, ldr, ws, Ly, ctr + 16, err, s, target, &ks_x, nullptr, nullptr, 0,
+                                       RwT + lcs, ldr, ws, Ly, ctr + 16, err, s, lc, &ks_x, nullptr, nullptr, 0,
                                        nullptr, ar));
                 launch_dist_psum<T>((const T *)(ws + Ly.part), ks_x, Ly.mp, mx, ar + 256 * 32, s);
             } else {
@@ -572,7 +589,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         const int k1 = k0 + NBMAX * 32;
         {
             PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
-            launch_k_prep<T>(false, prep_grid(pa, api_apply_target()), pa, s);
+            launch_k_prep<T>(false, prep_grid(pa, lc), pa, s);
             BD_HIP(hipGetLastError());
         }
         const long lck = (long)dist_panels_before(k1 / 32, P, me) * 32;

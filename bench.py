@@ -89,6 +89,11 @@ def parse():
     p.add_argument("--lanes", type=int, default=None,
                    help="pipelined: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
                         "(default 8; across GPUs each lane has its own RCCL communicator)")
+    p.add_argument("--s2-lanes", type=int, default=None,
+                   help="pipelined, one GPU: stage-2 streams (matrix j's stage 2 on stream j mod S2L; "
+                        "default: one per lane)")
+    p.add_argument("--s2-priority", choices=["normal", "high"], default="normal",
+                   help="pipelined: HIP priority of the stage-2 streams")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -429,13 +434,15 @@ def main():
     # stream has a queue).  Read when the HIP runtime initialises, so set first;
     # raised (never lowered) from whatever the environment holds (4 on the
     # MI355X pool, HIP's own default).
+    if args.s2_lanes is None:
+        args.s2_lanes = args.lanes
     if args.lanes > 1:
         # (across GPUs every lane's stage-1 stream also carries an RCCL
         # communicator with internal streams of its own; giving them queues
         # too -- all 32 -- was measured slower at world size 1, N = 8192:
         # 11.95 vs 15.30 TFLOP/s distributed and 16.9 vs 21.1 single-GPU in
         # the same process, profiles/r04_hwq_ab.txt)
-        want = min(32, 2 * args.lanes + 4)
+        want = min(32, args.lanes + args.s2_lanes + 4)
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
@@ -481,10 +488,11 @@ def main():
     if args.s2_cus is not None:
         s2_cus = args.s2_cus
     lanes = args.lanes if pipelined else 1
-    if pipelined and lanes * max(s2_cus, 1) > torch.cuda.get_device_properties(dev).multi_processor_count:
-        # every lane's stage-2 kernel is a persistent grid of s2_cus workgroups,
-        # one per CU: together they must fit the chip
-        sys.exit(f"bench.py: lanes * s2_cus = {lanes} * {s2_cus} exceeds the device's CUs")
+    s2_lanes = (args.s2_lanes if not dist_mode else lanes) if pipelined else 1
+    if pipelined and s2_lanes * max(s2_cus, 1) > torch.cuda.get_device_properties(dev).multi_processor_count:
+        # every stage-2 stream's kernel is a persistent grid of s2_cus
+        # workgroups, one per CU: together they must fit the chip
+        sys.exit(f"bench.py: stage-2 streams * s2_cus = {s2_lanes} * {s2_cus} exceeds the device's CUs")
     S.set_overlap(s2_cus)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -505,7 +513,7 @@ def main():
     # GPUs a matrix's stage 1 is a chain of per-panel collectives and factors,
     # so more matrices in flight hide more of it.
     sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
-    sb_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    sb_l = [torch.cuda.Stream(dev, priority=-1 if args.s2_priority == "high" else 0) for _ in range(s2_lanes)]
     if dist_mode:
         from svdsolver_amd import dist as D
         for s_a in sa_l:   # one communicator per lane's stage-1 stream
@@ -577,7 +585,7 @@ def main():
         for i in range(count):
             j = first + i
             A = mats[j]
-            s_a, s_b = sa_l[j % nl], sb_l[j % nl]
+            s_a, s_b = sa_l[j % nl], sb_l[j % (s2_lanes if mode["pipe"] else 1)]
             with torch.cuda.stream(s_a):
                 if not mode["pipe"] and last is not None:
                     s_a.wait_event(last)
@@ -711,7 +719,8 @@ def main():
                                        if dist_mode else f"replicas{world}"),
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
                                     if pipelined else "off: one reduction at a time"),
-                       "stage2_cus": s2_cus or "all", "lanes": lanes,
+                       "stage2_cus": s2_cus or "all", "lanes": lanes, "stage2_streams": s2_lanes,
+                       "stage2_priority": args.s2_priority,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},
             "latency_ms_per_reduction": round(s1 + s2, 3),

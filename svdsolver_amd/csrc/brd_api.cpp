@@ -104,6 +104,7 @@ struct Pending {
     std::string kind;
     hipEvent_t a, b;
     double flops, bytes;
+    int grid = 0;   // workgroups (0: unknown), for the launch timeline
 };
 
 struct Ctx {
@@ -134,6 +135,11 @@ struct Ctx {
     int *s2_err_host = nullptr;  // pinned copy of an error word
     int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
+    // BRD_PROF_TRACE=<file>: every profiled launch appended as "kind grid
+    // start_ms end_ms" relative to the event recorded at brd_profile_enable
+    // (developer timeline of a stream: tools/cu_time.py --lib)
+    FILE *trace = nullptr;
+    hipEvent_t trace_ref = nullptr;
     // events armed for the next launch (ProfScope in launch mode)
     hipEvent_t ext_a = nullptr, ext_b = nullptr;
     bool ext_armed = false, ext_taken = false;
@@ -383,6 +389,12 @@ static void prof_drain() {
         hipEventSynchronize(p.b);
         float ms = 0;
         hipEventElapsedTime(&ms, p.a, p.b);
+        if (g_ctx.trace && g_ctx.trace_ref) {
+            float t0 = 0, t1 = 0;
+            hipEventElapsedTime(&t0, g_ctx.trace_ref, p.a);
+            hipEventElapsedTime(&t1, g_ctx.trace_ref, p.b);
+            fprintf(g_ctx.trace, "%s %d %.4f %.4f\n", p.kind.c_str(), p.grid, t0, t1);
+        }
         ProfAcc &a = g_ctx.acc[p.kind];
         a.launches += 1;
         a.ms += ms;
@@ -532,9 +544,9 @@ void api_prof_end(void *h, hipStream_t s) {
 // Launch-mode profiling for kernels launched outside a ProfScope (the blocked
 // stage 1): two events the caller hands to hipExtLaunchKernel, queued for
 // prof_drain.  False (no events) when profiling is off.
-bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b) {
+bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b, int grid) {
     if (!g_ctx.prof) return false;
-    Pending p{kind, get_event(), get_event(), flops, bytes};
+    Pending p{kind, get_event(), get_event(), flops, bytes, grid};
     *a = p.a;
     *b = p.b;
     g_ctx.pending.push_back(p);
@@ -770,6 +782,18 @@ int brd_use_own_stream(void) {
 int brd_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(brd::g_ctx.mu);
     brd::g_ctx.prof = enable != 0;
+    const char *tp = getenv("BRD_PROF_TRACE");
+    if (enable && tp && !brd::g_ctx.trace) {
+        brd::g_ctx.trace = fopen(tp, "w");
+        if (!brd::g_ctx.trace_ref) hipEventCreate(&brd::g_ctx.trace_ref);
+        hipDeviceSynchronize();
+        hipEventRecord(brd::g_ctx.trace_ref, nullptr);
+    }
+    if (!enable && brd::g_ctx.trace) {
+        brd::prof_drain();
+        fclose(brd::g_ctx.trace);
+        brd::g_ctx.trace = nullptr;
+    }
     return BRD_OK;
 }
 

@@ -398,7 +398,31 @@ struct GemmArgs {
     int ntiles;                     // tiles
     int nfull = 0, nh = 0;          // k_blkupd_p: nh > 0: tiles [0, nfull) whole, then
                                     // nh half tiles (64 rows) of tiles nfull, nfull + 1, ...
+    int xsr = 0, xsc = 0;           // k_blkupd_p: > 0: per-XCD super-tiles of xsr x xsc tiles
+                                    // (xsr xsc = grid / 8; blkupd_tile), else row-major order
 };
+
+// k_blkupd_p's tile order.  Tile q of the order -> (tile row, tile column).
+// With super-tiles (xsr > 0) the full xsr x xsc blocks come first, each one's
+// tiles row-major, then the right strip and the bottom strip row-major;
+// otherwise row-major.
+__host__ __device__ inline void blkupd_tile(const GemmArgs &a, int q, int &tr, int &tc) {
+    if (a.xsr <= 0) { tr = q / a.tiles_c; tc = q % a.tiles_c; return; }
+    const int tiles_r = a.ntiles / a.tiles_c, nsc = a.tiles_c / a.xsc;
+    const int Rf = (tiles_r / a.xsr) * a.xsr, Cf = nsc * a.xsc, per = a.xsr * a.xsc;
+    if (q < Rf * Cf) {
+        const int st = q / per, w = q - st * per;
+        tr = (st / nsc) * a.xsr + w / a.xsc;
+        tc = (st % nsc) * a.xsc + w % a.xsc;
+        return;
+    }
+    int e = q - Rf * Cf;
+    const int rw = a.tiles_c - Cf;
+    if (e < Rf * rw) { tr = e / rw; tc = Cf + e % rw; return; }
+    e -= Rf * rw;
+    tr = Rf + e / a.tiles_c;
+    tc = e % a.tiles_c;
+}
 
 // ---- LDS-DMA and raw buffer accesses (k_blkupd_p, k_rpass_d) -----------------
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -452,7 +476,7 @@ template <typename F, typename... Args>
 static inline void blk_launch(const char *kind, double flops, double bytes, F kernel, dim3 grid, dim3 block,
                               hipStream_t s, Args... args) {
     hipEvent_t ea, eb;
-    if (api_prof_launch_events(kind, flops, bytes, &ea, &eb))
+    if (api_prof_launch_events(kind, flops, bytes, &ea, &eb, (int)(grid.x * grid.y)))
         hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ea, eb, 0, args...);
     else
         hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);

@@ -200,8 +200,25 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
         u32x4_t ra, rb;
         unsigned va[2], vb[2];
     };
-    auto dma_of = [&](int t) {
+    // Position p of the persistent walk (round p / G, workgroup p % G) -> tile.
+    // With super-tiles, a full round's G tiles are dealt so that the G / 8
+    // workgroups of one XCD (workgroup b runs on XCD b mod 8) take one
+    // super-tile: its Lw rows and RwT columns (xsr + xsc strips of 256 KB)
+    // stay in that XCD's 4 MB L2.
+    const int G0 = gridDim.x;
+    auto tile_at = [&](int p) {
+        int q = p;
+        if (a.xsr > 0) {
+            const int r = p / G0, b = p - r * G0;
+            if ((r + 1) * G0 <= a.nfull) q = r * G0 + (b & 7) * (G0 >> 3) + (b >> 3);
+        }
+        int tr, tc;
+        blkupd_tile(a, q, tr, tc);
+        return tr * a.tiles_c + tc;
+    };
+    auto dma_of = [&](int p) {
         Dma d;
+        const int t = tile_at(p);
         const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
         d.ra = rsrc_of(Lw + (size_t)r0 * 256);
         d.rb = rsrc_of(RwT + c0);
@@ -299,7 +316,8 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
     }
     int tix = 0;
     for (int t = blockIdx.x; t < nfull; t += gridDim.x, ++tix) {
-        const int r0 = (t / a.tiles_c) * kGM, c0 = (t % a.tiles_c) * kGM;
+        const int tt = tile_at(t);
+        const int r0 = (tt / a.tiles_c) * kGM, c0 = (tt % a.tiles_c) * kGM;
         const Cio ccur = cio_of(r0, c0, wr);
         const bool more = t + (int)gridDim.x < nfull;
         const Dma dnext = dma_of(more ? t + gridDim.x : t);
@@ -396,8 +414,9 @@ __global__ void __launch_bounds__(kGT2, 1) k_blkupd_p(GemmArgs a) {
         }
     };
     for (int h = h0; h < a.nh; h += G) {
-        const int t = nfull + (h >> 1);
-        const int r0 = (t / a.tiles_c) * kGM + (h & 1) * 64, c0 = (t % a.tiles_c) * kGM;
+        const int t = nfull + (h >> 1);   // positions past the full rounds keep their order
+        const int tt = tile_at(t);
+        const int r0 = (tt / a.tiles_c) * kGM + (h & 1) * 64, c0 = (tt % a.tiles_c) * kGM;
         if (r0 >= a.rows) continue;   // the lower half of a tile past the matrix (uniform)
         // Lw: granule column kg = w of rows lane ^ kg, stored at row lane;
         // RwT as for the whole tile
@@ -474,7 +493,20 @@ void launch_k_blkupd(dim3 grid, const GemmArgs &g, hipStream_t s, double fl, dou
                 gs.nh = 2 * r;
             }
             const int items = gs.nh > 0 ? gs.nfull + gs.nh : g.ntiles;
-            blk_launch("s1_blkupd", fl, by, k_blkupd_p<T>, dim3(std::min<int>(items, tgt)), dim3(kGT2), s, gs);
+            const int grid = std::min<int>(items, tgt);
+            if (gs.nh == 0) gs.nfull = g.ntiles;
+            // per-XCD super-tiles (blkupd_tile) when the grid deals whole rounds
+            // evenly over the 8 XCDs: 4 x (grid / 32) tiles, e.g. 4 x 8 on 256
+            // CUs, 4 x 7 beside a 32-CU stage-2 reservation.  BRD_BLKUPD_XCD=0 /
+            // 1 (A/B)
+            const char *xe = getenv("BRD_BLKUPD_XCD");
+            const int tiles_r = g.ntiles / g.tiles_c;
+            gs.xsr = gs.xsc = 0;
+            if ((xe ? atoi(xe) : 0) && grid % 32 == 0 && gs.nfull >= grid && tiles_r >= 4 && g.tiles_c >= grid / 32) {
+                gs.xsr = 4;
+                gs.xsc = grid / 32;
+            }
+            blk_launch("s1_blkupd", fl, by, k_blkupd_p<T>, dim3(grid), dim3(kGT2), s, gs);
             return;
         }
     }

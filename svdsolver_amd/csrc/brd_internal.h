@@ -125,7 +125,7 @@ int api_min_run(int level);                        // least slabs per apply work
 bool api_overlap_active();                         // brd_set_overlap reservation in force
 void *api_prof_begin(const char *kind, double flops, double bytes, hipStream_t s);
 void api_prof_end(void *handle, hipStream_t s);
-bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b);
+bool api_prof_launch_events(const char *kind, double flops, double bytes, hipEvent_t *a, hipEvent_t *b, int grid = 0);
 // Profiling with kernel-bracketing events: a ProfScope in "launch" mode arms a
 // pair of events that the NEXT stage-1 launch takes (hipExtLaunchKernel
 // records them at the dispatch's start and end, the timestamps rocprofv3

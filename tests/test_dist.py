@@ -391,16 +391,20 @@ def _edge_worker(rank, world, port, n, b, kind, out_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,n", [(2, 512), (3, 512), (8, 2048)])
 @pytest.mark.parametrize("kind", ["rank1_exact", "rank20_exact", "dup_rows", "zero_col_in_panel"])
-def test_distributed_structured_panels(world, kind, tmp_path):
+def test_distributed_structured_panels(world, n, kind, tmp_path):
     """Exactly rank-deficient row panels on the sharded CholeskyQR (ADVICE r4:
     the completion vectors of sCQR3's middle pass, k_cqr_mid, must keep the
     transform orthogonal when the panel's rows are spread over ranks): the
     gathered band keeps exact zeros outside it and the input's singular
-    values (fp64, 1e-12 sigma_max), as on one GPU (test_gpu_edges.py)."""
+    values (fp64, 1e-12 sigma_max), as on one GPU (test_gpu_edges.py).  At
+    P = 8, n = 2048 the deficient panels' single CholeskyQR pass
+    on the completed y (one pass where cqr_shifted_pass makes two) runs over
+    rows spread across 8 ranks and 508..32 rows each: a transform off
+    orthogonality by more than ~1e-12 would show in the singular values."""
     import torch.multiprocessing as mp
-    n, b = 512, 32
+    b = 32
     out = str(tmp_path / "band.npy")
     mp.spawn(_edge_worker, args=(world, _free_port(), n, b, kind, out), nprocs=world, join=True)
     band = np.load(out)

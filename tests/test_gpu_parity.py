@@ -374,9 +374,26 @@ def test_reduce_many_pipelined_matches_serial(S, lanes):
     finally:
         S.set_overlap(0)
     for M, ref_band in zip(mats, bands):
-        B = M.cpu().numpy()   # signed: a sign flip in the band is an error
-        assert np.max(np.abs(B - ref_band)) <= 1e-13 * np.max(np.abs(ref_band))
+        B = M.cpu().numpy()   # signed up to the reduction's sign freedom
+        assert np.max(np.abs(_canon_signs(B) - _canon_signs(ref_band))) <= 1e-13 * np.max(np.abs(ref_band))
         assert np.all(B[~inb] == 0)
+
+
+def _canon_signs(B):
+    """The band up to the sign freedom of a two-sided orthogonal reduction,
+    B = D_L R D_R (D diagonal +-1): rows and columns flipped so that every
+    diagonal entry and every first superdiagonal entry is >= 0 (row i fixes
+    B[i, i], then column i + 1 fixes B[i, i + 1]).  Two bands that agree after
+    this differ only by the QR / LQ sign choices; any other sign change stays
+    visible."""
+    B = np.array(B, dtype=np.float64, copy=True)
+    n = B.shape[0]
+    for i in range(n):
+        if B[i, i] < 0:
+            B[i, :] = -B[i, :]
+        if i + 1 < n and B[i, i + 1] < 0:
+            B[:, i + 1] = -B[:, i + 1]
+    return B
 
 
 def test_stage1_f32_overlap_matches_serial(S):
@@ -410,8 +427,11 @@ def test_stage1_f32_overlap_matches_serial(S):
     inb = (j >= i) & (j - i <= b)
     for M, R in zip(mats, ref):
         B = M.cpu().numpy()
-        # signed: the sign choices come from the LU pivots, |pivot| >= 1
-        assert np.max(np.abs(B - R)) <= 2e-6 * np.max(np.abs(R))
+        # signed up to the reduction's sign freedom: the modified
+        # LU's s_j = -sign(q_jj) may differ where q_jj is near 0 (fp32 rounding
+        # differs between the stream's and the serial K splits), which flips a
+        # row / column of the band and nothing else
+        assert np.max(np.abs(_canon_signs(B) - _canon_signs(R))) <= 2e-6 * np.max(np.abs(R))
         assert np.all(B[~inb] == 0)
 
 
@@ -549,6 +569,30 @@ def test_blkupd_half_tiles_bitwise(S, m, n, T):
             os.environ.pop("BRD_BLKUPD_HALF", None)
         else:
             os.environ["BRD_BLKUPD_HALF"] = old
+    assert np.array_equal(B0, B1)
+
+
+@pytest.mark.parametrize("m,n,T", [(2304, 2304, "double"), (3000, 2900, "double"), (2600, 2600, "float")])
+def test_blkupd_xcd_order_bitwise(S, m, n, T):
+    """k_blkupd_p's per-XCD super-tile order (BRD_BLKUPD_XCD=1: a full round's
+    tiles dealt so each XCD's workgroups take one 4 x (grid / 32) block) gives
+    the band of the row-major order BIT FOR BIT: only which CU computes a
+    tile changes.  Sizes with >= one full round (>= 256 tiles) plus ragged
+    right / bottom strips and a half-tile last round."""
+    import os
+    rng = np.random.default_rng(7 * m + n)
+    A = (rng.random((m, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get("BRD_BLKUPD_XCD")
+    try:
+        os.environ["BRD_BLKUPD_XCD"] = "0"
+        B0 = S.brd_p1(A, 32)
+        os.environ["BRD_BLKUPD_XCD"] = "1"
+        B1 = S.brd_p1(A, 32)
+    finally:
+        if old is None:
+            os.environ.pop("BRD_BLKUPD_XCD", None)
+        else:
+            os.environ["BRD_BLKUPD_XCD"] = old
     assert np.array_equal(B0, B1)
 
 

@@ -94,6 +94,12 @@ def parse():
                         "default: one per lane)")
     p.add_argument("--s2-priority", choices=["normal", "high"], default="normal",
                    help="pipelined: HIP priority of the stage-2 streams")
+    p.add_argument("--drain", choices=["on", "off"], default="on",
+                   help="pipelined, one GPU: the last round's stage 2s (the drain, no stage 1 left to run) "
+                        "each on a stream of its own once every earlier stage 2 is done, the CUs split "
+                        "evenly among them (at most the usual reservation each)")
+    p.add_argument("--s1-high", type=int, default=0,
+                   help="pipelined: the first S1H stage-1 streams at high HIP priority (A/B)")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -346,6 +352,14 @@ def stage2_roofline(sw, n, b, dtype, steps):
             "chain_bound_note": "about 4 dependent windows per sweep (lag-3 rule, DESIGN.md Stage 2)"}
 
 
+def plan_lanes(k: int, lmax: int = 10) -> int:
+    """Stage-1 lanes for a stream of k matrices: the fewest rounds that
+    lmax lanes allow, dealt evenly (k = 20 -> 10 lanes x 2 rounds; 12 -> 6 x
+    2; 5 -> 5 x 1)."""
+    rounds = max(1, -(-k // lmax))
+    return max(1, -(-k // rounds))
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -426,23 +440,33 @@ def single_gpu_same_n(S, torch, dev, n, b, tdt, steps, warmup, lanes, s2_cus, si
 
 def main():
     args = parse()
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.force_dist
     if args.lanes is None:
-        args.lanes = 8 if args.pipeline == "on" else 1
+        # one GPU: the K matrices dealt in balanced rounds over at most 10
+        # stage-1 lanes (K = 20: 2 rounds of 10), so no round runs with part
+        # of the lanes idle, and half as many stage-2 streams (a burst of
+        # finished stage 1s queues there instead of taking 32 CUs each).
+        # Same box, N = 8192 fp64, 20 steps: 8 lanes / 8 stage-2 streams (round
+        # 5: 3+3+3+3+2+2+2+2 matrices) 25.12 / 25.08 TFLOP/s; 10 / 5 26.59 /
+        # 26.73 / 26.70; 10 / 6 26.67; 10 / 4 26.06; 10 / 10 (24 CUs each)
+        # 26.05; 12 / 6 26.15; 5 / 5 22.9; 20 / 8 25.8 (gpurun_out r6d / r6e,
+        # profiles/r06_lanes_ab.txt).  Across GPUs: 8 lanes (one communicator each).
+        args.lanes = (8 if multi else plan_lanes(args.steps)) if args.pipeline == "on" else 1
+    if args.s2_lanes is None:
+        args.s2_lanes = args.lanes if multi else max(1, (args.lanes + 1) // 2)
     # Every lane launches on two HIP streams; with the runtime's default of 4
     # hardware queues per process, streams beyond that share a queue and
     # their work serialises (measured: 2 lanes 14.1 -> 17.8 TFLOP/s once each
     # stream has a queue).  Read when the HIP runtime initialises, so set first;
     # raised (never lowered) from whatever the environment holds (4 on the
     # MI355X pool, HIP's own default).
-    if args.s2_lanes is None:
-        args.s2_lanes = args.lanes
     if args.lanes > 1:
         # (across GPUs every lane's stage-1 stream also carries an RCCL
         # communicator with internal streams of its own; giving them queues
         # too -- all 32 -- was measured slower at world size 1, N = 8192:
         # 11.95 vs 15.30 TFLOP/s distributed and 16.9 vs 21.1 single-GPU in
         # the same process, profiles/r04_hwq_ab.txt)
-        want = min(32, args.lanes + args.s2_lanes + 4)
+        want = min(32, args.lanes + args.s2_lanes + 4 + (args.lanes if (args.drain == "on" and not multi) else 0))
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
@@ -512,7 +536,7 @@ def main():
     # world size 1 over RCCL (--force-dist, 12 steps), 14.6 vs 16.0 -- across
     # GPUs a matrix's stage 1 is a chain of per-panel collectives and factors,
     # so more matrices in flight hide more of it.
-    sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    sa_l = [torch.cuda.Stream(dev, priority=-1 if l < args.s1_high else 0) for l in range(lanes)]
     sb_l = [torch.cuda.Stream(dev, priority=-1 if args.s2_priority == "high" else 0) for _ in range(s2_lanes)]
     if dist_mode:
         from svdsolver_amd import dist as D
@@ -575,6 +599,16 @@ def main():
                 S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
 
+    # The drain (one GPU, pipelined): once the last round's stage 1s are
+    # issued no stage-1 work is left to share the chip with, so each of the
+    # last `lanes` matrices' stage 2 gets a stream of its own (after every
+    # earlier stage 2, so at most `lanes` sweep grids are resident) and an
+    # equal share of the CUs (min(s2_cus, CUs / lanes) workgroups) instead of
+    # queueing two deep behind the s2_lanes streams.
+    dev_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    use_drain = args.drain == "on" and pipelined and not dist_mode and args.stages == "12" and s2_lanes < lanes
+    sd_l = [torch.cuda.Stream(dev) for _ in range(lanes)] if use_drain else []
+
     def issue(first, count, ev=None):
         last = None
         # one reduction at a time: lane 0 only.  Matrices queued on the other
@@ -582,10 +616,23 @@ def main():
         # parked on barriers slow the dispatch of the active one (measured:
         # stage 1 137 ms vs 89 ms with 4 lanes' streams waiting).
         nl = lanes if mode["pipe"] else 1
+        nd = min(lanes, count) if (use_drain and mode["pipe"]) else 0
+        drain_cus = max(1, min(s2_cus, dev_cus // max(nd, 1)))
+        before = []   # events: every stage 2 issued before the drain
         for i in range(count):
             j = first + i
             A = mats[j]
             s_a, s_b = sa_l[j % nl], sb_l[j % (s2_lanes if mode["pipe"] else 1)]
+            drain = i >= count - nd
+            if drain:
+                if not before:
+                    for q in sb_l:
+                        e_ = torch.cuda.Event()
+                        e_.record(q)
+                        before.append(e_)
+                s_b = sd_l[i - (count - nd)]
+                for e_ in before:
+                    s_b.wait_event(e_)
             with torch.cuda.stream(s_a):
                 if not mode["pipe"] and last is not None:
                     s_a.wait_event(last)
@@ -598,7 +645,11 @@ def main():
                 s_b.wait_event(e1)
                 if ev:
                     ev[i][1].record(s_b)
+                if drain:
+                    S.set_overlap(drain_cus)
                 stage2(A, j)
+                if drain:
+                    S.set_overlap(s2_cus)
                 last = torch.cuda.Event(enable_timing=bool(ev))
                 last.record(s_b)
                 if ev:
@@ -720,6 +771,8 @@ def main():
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
                                     if pipelined else "off: one reduction at a time"),
                        "stage2_cus": s2_cus or "all", "lanes": lanes, "stage2_streams": s2_lanes,
+                       "drain": ("the last round's stage 2s on streams of their own, the CUs split among them"
+                                 if use_drain else "off"),
                        "stage2_priority": args.s2_priority,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},

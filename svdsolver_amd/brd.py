@@ -326,7 +326,7 @@ def overlap_cus(n: int) -> int:
 
 
 def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = None, sync: bool = True,
-                lanes: int = 1):
+                lanes: int = 1, s2_lanes: Optional[int] = None):
     """Two-stage reduction of a sequence of square CUDA tensors, each in place,
     pipelined over pairs of HIP streams ("lanes"): on a lane, stage 2 of
     matrix i (its own stream, ``s2_cus`` workgroups) runs beside stage 1 of the
@@ -335,8 +335,11 @@ def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = No
     tensors).  Each matrix sees exactly the calls of ge2band + band2bd; only
     their overlap differs.  The library's overlap setting is restored on exit.
     More than one lane pays only with one hardware queue per stream: set
-    GPU_MAX_HW_QUEUES >= 2 * lanes + 4 (at most 32) before HIP initialises
-    (DESIGN.md, "lanes").
+    GPU_MAX_HW_QUEUES >= lanes + s2_lanes + 4 (at most 32) before HIP
+    initialises ("lanes").  ``s2_lanes``: stage-2 streams (matrix
+    i's stage 2 on stream i mod s2_lanes; default one per lane): fewer than
+    the lanes make a burst of finished stage 1s queue for the sweep instead of
+    each taking ``s2_cus`` CUs at once (bench.py: 10 lanes, 5 stage-2 streams).
     """
     import torch
     if not mats:
@@ -346,23 +349,24 @@ def reduce_many(mats, b: int, *, sigma: bool = False, s2_cus: Optional[int] = No
     dev = mats[0].device
     cus = overlap_cus(mats[0].shape[0]) if s2_cus is None else int(s2_cus)
     lanes = min(int(lanes), len(mats))
+    s2l = lanes if s2_lanes is None else max(1, min(int(s2_lanes), len(mats)))
     # every lane's stage-2 kernel is a persistent grid of ``cus`` workgroups,
     # one per CU (its LDS ring takes the CU), whose bundles wait on each
     # other: with more workgroups in flight than the chip holds, a partly
     # resident grid stalls ("Overlap and lanes")
     dev_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    if lanes * cus > dev_cus:
-        raise ValueError(f"lanes * s2_cus = {lanes} * {cus} exceeds the device's {dev_cus} CUs "
+    if s2l * cus > dev_cus:
+        raise ValueError(f"stage-2 streams * s2_cus = {s2l} * {cus} exceeds the device's {dev_cus} CUs "
                          "(stage-2 grids must fit the chip together)")
     s_a = [torch.cuda.Stream(dev) for _ in range(lanes)]
-    s_b = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    s_b = [torch.cuda.Stream(dev) for _ in range(s2l)]
     for s in s_a:
         s.wait_stream(torch.cuda.current_stream(dev))
     out = []
     set_overlap(cus)
     try:
         for i, A in enumerate(mats):
-            sa, sb = s_a[i % lanes], s_b[i % lanes]
+            sa, sb = s_a[i % lanes], s_b[i % s2l]
             with torch.cuda.stream(sa):
                 ge2band(A, b, sync=False)
                 done1 = torch.cuda.Event()

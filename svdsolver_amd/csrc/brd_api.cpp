@@ -136,7 +136,7 @@ struct Ctx {
     int overlap_cus = 0;         // > 0: stage 2 on this many CUs, stage 1 sized for the rest
     bool prof = false;
     // BRD_PROF_TRACE=<file>: every profiled launch appended as "kind grid
-    // start_ms end_ms" relative to the event recorded at brd_profile_enable
+    // start_ms end_ms bytes" relative to the event recorded at brd_profile_enable
     // (developer timeline of a stream: tools/cu_time.py --lib)
     FILE *trace = nullptr;
     hipEvent_t trace_ref = nullptr;
@@ -393,7 +393,7 @@ static void prof_drain() {
             float t0 = 0, t1 = 0;
             hipEventElapsedTime(&t0, g_ctx.trace_ref, p.a);
             hipEventElapsedTime(&t1, g_ctx.trace_ref, p.b);
-            fprintf(g_ctx.trace, "%s %d %.4f %.4f\n", p.kind.c_str(), p.grid, t0, t1);
+            fprintf(g_ctx.trace, "%s %d %.4f %.4f %.0f\n", p.kind.c_str(), p.grid, t0, t1, p.bytes);
         }
         ProfAcc &a = g_ctx.acc[p.kind];
         a.launches += 1;

@@ -383,7 +383,7 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 // layout: global column panel p on rank p mod P).  Lw = [V | X] (m x 256) is
 // replicated, RwT = [Y | U] and Ub hold this rank's columns; the block update
 // k_blkupd is local to each rank's columns.  Per panel j (global panel p,
-// column c), three collectives:
+// column c), five collectives:
 //   QR   the owner of panel p forms the corrected column panel (k_prep_qr,
 //        after every rank has added X_{j-1} to its Lw from the all-reduced
 //        X partials) and runs its CholeskyQR; V' = Q (m - c rows), Q_t and
@@ -401,13 +401,15 @@ template hipError_t blk_ge2band<float>(float *, int, int, long, void *, hipStrea
 //        -- and the local Q = P R^-1; three all-gathers per panel (G1, G2 and
 //        sCQR3's middle Gram).  The rank holding panel p+1 (the band block's
 //        columns: the panel's top block) finishes the basis-kernel
-//        reconstruction inline (LU of Q_t - S, S_j, the band block) and
-//        BROADCASTS S_j (32 x 32).  U_j's rows stay where they were formed.
+//        reconstruction inline (LU of Q_t - S, S_j, the band block), S_j
+//        straight into its slot of the X all-reduce below (the other ranks
+//        zero it, so the sum is S_j exactly; round 5 broadcast it on its
+//        own).  U_j's rows stay where they were formed.
 //   X    X_j = A U_j S_j sums over columns: each rank's split-K partials
 //        (and its part of G = Rw^T U_j) are summed locally (k_dist_psum) and
-//        ALL-REDUCED (m - c - 32 + 256 rows of 32).
+//        ALL-REDUCED (m - c - 32 + 256 rows of 32, and S_j).
 // Message sizes per panel: m x 32 (broadcast), 3 x P x 8 KB (all-gathers),
-// 8 KB (broadcast of S_j), (m + 256) x 32 (all-reduce) -- against the
+// (m + 256) x 32 + 1024 (all-reduce) -- against the
 // per-panel path's m x b broadcast + P b^2 gather + b x m all-reduce, but 2.5
 // passes over the trailing matrix per 32 columns instead of 4, the update on
 // the matrix cores.  With one rank every collective is the identity and the
@@ -424,7 +426,7 @@ DistBlk dist_blk_layout(int m, int n, int P, int rank, size_t elem) {
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     D.bc = take((size_t)m * 32 * elem + 1032 * sizeof(double));   // V' rows, then Q_t + zero flag
     D.rec = take((size_t)3 * P * kCqrRec * sizeof(double));       // the row panel QR's Gram records
-    D.ar = take(((size_t)m * 32 + 256 * 32) * elem);              // G (256 x 32), then X rows
+    D.ar = take(((size_t)m * 32 + 256 * 32 + 1024) * elem);       // G (256 x 32), X rows, then S_j
     D.total = off;
     return D;
 }
@@ -502,6 +504,7 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
         pa.gew = cw + 3072 * kCW;        // CqrWs::ew
         pa.gcnt = ctr + 64;
     };
+    const T *s_prev = nullptr;   // S_{j-1}: the previous panel's all-reduced slot
     for (int k0 = 0; k0 < kend; k0 += NBMAX * 32) {
         for (int j = 0; j < NBMAX; ++j) {
             const int p = k0 / 32 + j, c = 32 * p, mr = m - c, mx = m - c - 32;
@@ -511,12 +514,12 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             const long lcs = (long)dist_panels_before(p + 1, P, me) * 32;   // first local trailing column
             const int nc = n_loc - (int)lcs;                 // local trailing columns
             T *Tj = tf + 1024 * j, *Sj = tf + 1024 * (NBMAX + j);
+            T *sj_ar = ar + (size_t)mx * 32 + 256 * 32;   // S_j's slot at the tail of the X all-reduce
             double *qt = (double *)((char *)bc + (size_t)mr * 32 * sizeof(T));   // Q_t, zero flag
             // ---- X_{j-1} (every rank) + the column panel's QR (its owner) ----------
             const bool fold_qr = own && j > 0 && (foldm & 1);
             if (j > 0) {
-                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (NBMAX + j - 1), sg0,
-                                   lco);
+                PrepArgs pa = prep(c, j, mr, 1, own ? 1 : 0, ar + 256 * 32, 0, 1, ar, s_prev, sg0, lco);
                 if (fold_qr) gram_into(pa);
                 launch_k_prep<T>(false, prep_grid(pa, lc), pa, s);
                 BD_HIP(hipGetLastError());
@@ -559,8 +562,12 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                 a.goff = (long)((me - o2 + P) % P) * kCW * kCT;
                 a.top = own2 ? 1 : 0;
                 const int nwg = std::max(1, (a.M + kCT - 1) / kCT);
-                const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, Sj,
+                // S_j straight into its slot of the X all-reduce (the other
+                // ranks add exact zeros: the sum is S_j bit for bit), which
+                // replaces a broadcast of its own
+                const FinArgs fl{cws + cqr_ws_qt(), cws + cqr_ws_zero(), sgl + 32 * j, own2 ? sj_ar : Sj,
                                  own2 ? (void *)(A + (size_t)c * lda + lcs) : nullptr, 1, lda};
+                if (!own2) BD_HIP(hipMemsetAsync(sj_ar, 0, 1024 * sizeof(T), s));
                 const size_t rb = (size_t)kCqrRec * sizeof(double);
                 launch_k_cqr<T>(kCqrGram, nwg, a, fl, s);   // -> record bank 0: this rank's G1, exponent
                 BD_TRY(C.allgather(rec + (size_t)me * kCqrRec, rec, rb, s));
@@ -571,7 +578,6 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
                 // V rows into RwT and Ub; the top block's owner finishes inline (LU, S_j, the band block)
                 launch_k_cqr<T>(own2 ? kCqrVInline : kCqrV, nwg, a, fl, s);
                 BD_HIP(hipGetLastError());
-                BD_TRY(C.bcast(Sj, 1024 * sizeof(T), o2, s));
             }
             // ---- X pass (local columns), partials summed and all-reduced ------------
             if (nc > 0) {
@@ -583,12 +589,13 @@ int blk_ge2band_dist(T *A, int m, int n, long lda, Comm &C, void *wsv, hipStream
             } else {
                 BD_HIP(hipMemsetAsync(ar, 0, ((size_t)mx * 32 + 256 * 32) * sizeof(T), s));
             }
-            BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32, dt, s));
+            BD_TRY(C.allreduce_sum(ar, (size_t)mx * 32 + 256 * 32 + 1024, dt, s));
+            s_prev = sj_ar;   // read by the next prep_qr / the block end, before the next X pass writes ar
         }
         // ---- block end: X_3 (every rank), the rank-256 update of my columns ---------
         const int k1 = k0 + NBMAX * 32;
         {
-            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, tf + 1024 * (2 * NBMAX - 1), sg0, 0);
+            PrepArgs pa = prep(k1, NBMAX, m - k1, 1, 0, ar + 256 * 32, 0, 1, ar, s_prev, sg0, 0);
             launch_k_prep<T>(false, prep_grid(pa, lc), pa, s);
             BD_HIP(hipGetLastError());
         }

@@ -1221,6 +1221,12 @@ constexpr int kSweepWriters = 2;   // writer waves (batches dealt alternately)
 // fp64: 16 rows 156.2, 32 rows 146.0.  Between the two sizes (not measured)
 // the switch is at the midpoint.  BRD_S2_SWEEP_ROWS=16 / 32 forces either.
 constexpr int kSweepRowsSplitN = 12288;
+// The shrinking grid's stages (k_sweeps, SweepStages): the grid halves once
+// the bundles alive at once, (n - i) / (64 S) + 1, times kStageMargin plus
+// kStageSpare fit in half of it; at least kStageMin workgroups stay.
+// BRD_S2_STAGES=0 keeps the whole grid to the end (A/B).
+constexpr double kStageMargin = 1.25;
+constexpr int kStageSpare = 2, kStageMin = 4;
 static int sweep_rows_for(int n) {
     const char *e = getenv("BRD_S2_SWEEP_ROWS");   // (read per call: tests switch it)
     if (e && (atoi(e) == 16 || atoi(e) == 32)) return atoi(e);
@@ -1298,9 +1304,47 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The grid shrinks with the chain (a stage-2 reservation holds whole CUs, so
+// in a stream of reductions the CUs it no longer needs go back to stage 1).
+// A bundle of S sweeps starting at row i lives (n - i) / 32 task pairs and
+// bundles start 4 S tasks apart, so (n - i) / (64 S) bundles are alive at
+// once whatever the task time: ~43 at the top of an 8192 fp64 matrix, a few
+// near the bottom.  The host splits the bundles into stages (SweepStages:
+// bundles [B_k, B_k+1) on the first G_k workgroups, G_k halving from stage to
+// stage); in stage k bundle beta goes to workgroup beta mod G_k.  G_k divides
+// G_k-1, so a workgroup's next bundle is always >= G_k bundles after its last
+// one (consecutive bundles on different workgroups, as with one stage), and
+// workgroups >= G_k leave after stage k - 1.  The dealing is static: no
+// atomics on the chain's hand-offs.
+struct SweepStages {
+    int nst;          // stages (1: the whole chain on the grid)
+    int B[5];         // first bundle of each stage (B[0] = 0)
+    int G[4];         // workgroups of each stage (G[0] = the grid)
+};
+__device__ __forceinline__ int sweeps_next(const SweepStages &st, int w, int beta, int nbundles) {
+    int k = 0;
+    while (k + 1 < st.nst && beta >= st.B[k + 1]) ++k;
+    int nx = beta + st.G[k];
+    while (k + 1 < st.nst && nx >= st.B[k + 1]) {   // into the next stage
+        ++k;
+        if (w >= st.G[k]) return nbundles;          // not in it: leave
+        const int b0 = st.B[k];
+        nx = b0 + (((w - b0) % st.G[k]) + st.G[k]) % st.G[k];   // first beta >= B_k with beta = w mod G_k
+    }
+    return nx;
+}
+__device__ __forceinline__ int sweeps_first(const SweepStages &st, int w, int nbundles) {
+    for (int k = 0; k < st.nst; ++k) {
+        if (w >= st.G[k]) return nbundles;
+        const int b0 = st.B[k];
+        const int c = b0 + (((w - b0) % st.G[k]) + st.G[k]) % st.G[k];
+        if (c < st.B[k + 1]) return c;
+    }
+    return nbundles;
+}
 template <typename T, int WR>
 __global__ void __launch_bounds__(sweeps_max_threads<T>())
-k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
+k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *rows_done, int *err, SweepStages st)
 {
     constexpr int b = 32;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -1312,7 +1356,8 @@ k_sweeps(T *A, int n, long lda, int sigma, int S, int R, unsigned magic, int *ro
     const S2Ring<T> rg{ring, P, R, magic};
     const int nbundles = (n - 1 + S - 1) / S;
 
-    for (int beta = blockIdx.x; beta < nbundles; beta += gridDim.x) {
+    for (int beta = sweeps_first(st, (int)blockIdx.x, nbundles); beta < nbundles;
+         beta = sweeps_next(st, (int)blockIdx.x, beta, nbundles)) {
         const int i0 = beta * S;
         const int nsw = min(S, n - 1 - i0);
         if (threadIdx.x < 12) {
@@ -1769,6 +1814,31 @@ static int coresident_limit(const void *fn, int threads, size_t lds) {
     return per_cu * cus;
 }
 
+static SweepStages sweep_stages(int n, int S, int nbundles, int grid) {
+    SweepStages st{};
+    st.nst = 1;
+    st.B[0] = 0;
+    st.G[0] = grid;
+    st.B[1] = nbundles;
+    const char *e = getenv("BRD_S2_STAGES");   // (read per call: tests switch it)
+    if (e && atoi(e) == 0) return st;
+    int g = grid;
+    for (int beta = 0; beta < nbundles && st.nst < 4; ++beta) {
+        const double alive = (double)(n - beta * S) / (64.0 * S) + 1.0;
+        const int half = g / 2;
+        // (each stage at least one round of its workgroups)
+        if (half >= kStageMin && g % 2 == 0 && beta >= st.B[st.nst - 1] + g &&
+            alive * kStageMargin + kStageSpare <= half) {
+            st.B[st.nst] = beta;
+            st.G[st.nst] = half;
+            ++st.nst;
+            g = half;
+        }
+    }
+    st.B[st.nst] = nbundles;
+    return st;
+}
+
 // prog: n+1 ints (zeroed here); err: the caller's sticky error word (never
 // reset here: a nonzero value from an earlier launch stays visible).
 template <typename T>
@@ -1795,8 +1865,9 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         const int cap = coresident_limit(fn, (int)block.x, lds);
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
-        if (w32) hipLaunchKernelGGL((k_sweeps<T, 32>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
-        else     hipLaunchKernelGGL((k_sweeps<T, 16>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err);
+        const SweepStages st = sweep_stages(n, S, nbundles, grid);
+        if (w32) hipLaunchKernelGGL((k_sweeps<T, 32>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err, st);
+        else     hipLaunchKernelGGL((k_sweeps<T, 16>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err, st);
         return hipGetLastError();
     }
     const int W = fast32 ? s2_waves_per_sweep() : 1;

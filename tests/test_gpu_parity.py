@@ -646,9 +646,38 @@ def test_reduce_many_stage2_bitwise_under_contention(S):
             W = Bd.clone()
             d, e = S.band2bd(W, b, sigma=sigma)
             ref.append((d.clone(), e.clone()))
-        got = S.reduce_many([A.clone() for A in As], b, sigma=sigma, lanes=4)
-        for (d0, e0), (d1, e1) in zip(ref, got):
-            assert torch.equal(d0, d1) and torch.equal(e0, e1)
+        # four lanes, four stage-2 streams; then five lanes over two stage-2
+        # streams (bench.py's split: sweeps queue behind each other's)
+        for lanes, s2l in ((4, None), (5, 2)):
+            got = S.reduce_many([A.clone() for A in As], b, sigma=sigma, lanes=lanes, s2_lanes=s2l)
+            for (d0, e0), (d1, e1) in zip(ref, got):
+                assert torch.equal(d0, d1) and torch.equal(e0, e1)
+
+
+@pytest.mark.parametrize("n,dt", [(2048, "f64"), (4100, "f32"), (8192, "f64")])
+def test_stage2_shrinking_grid_bitwise(S, n, dt, monkeypatch):
+    """k_sweeps' shrinking grid (SweepStages: the bundles dealt over 32, 16,
+    8, 4 workgroups as the chain's live bundles fall) changes only which
+    workgroup runs a bundle, never the arithmetic or the hand-off order: the
+    bidiagonal is the one-stage grid's bit for bit, beside a stage-2
+    reservation (32 workgroups, the stream's grid) and without one."""
+    import torch
+    b = 32
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    A = torch.from_numpy(np.random.default_rng(n).uniform(0, 5, (n, n))).to(tdt).cuda()
+    S.ge2band(A, b)
+    for cus in (0, S.overlap_cus(n)):
+        out = []
+        S.set_overlap(cus)
+        try:
+            for stages in ("0", "1"):
+                monkeypatch.setenv("BRD_S2_STAGES", stages)
+                W = A.clone()
+                d, e = S.band2bd(W, b)
+                out.append((d.clone(), e.clone()))
+        finally:
+            S.set_overlap(0)
+        assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]), cus
 
 
 @pytest.mark.parametrize("dt", ["f64", "f32"])

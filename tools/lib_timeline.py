@@ -15,7 +15,7 @@ CUS = int(sys.argv[3]) if len(sys.argv) > 3 else 256
 S2 = int(sys.argv[4]) if len(sys.argv) > 4 else 32
 rows = []
 for ln in open(path):
-    k, g, a, b = ln.split()
+    k, g, a, b = ln.split()[:4]
     g = int(g) or (S2 if k.startswith("s2") else 1)
     rows.append((float(a), float(b), k, min(g, CUS)))
 T0 = min(a for a, _, _, _ in rows)

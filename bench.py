@@ -24,10 +24,12 @@ its own matrices (weak scaling).  The step time is the max over ranks and
 `value` is the whole-job GFLOP/s.
 
 What `value` measures (config.value_kind): the throughput of a STREAM of
-independent reductions -- K matrices (default 20) issued back to back on 8
-lanes of HIP stream pairs (matrix j on lane j mod 8, stage 2 of a lane's
-matrix beside stage 1 of its next one; `--pipeline on`, the default),
-fill and drain inside the timed region.  The same K steps one reduction at a
+independent reductions -- K matrices (default 20) issued back to back on L
+stage-1 streams ("lanes", matrix j on lane j mod L; one GPU: K dealt in
+balanced rounds of at most 10, plan_lanes) and ceil(L / 2) stage-2 streams
+(matrix j's stage 2 on stream j mod that, after its stage 1, beside the
+following matrices' stage 1; `--pipeline on`, the default), fill and drain
+inside the timed region.  The same K steps one reduction at a
 time on one lane (the reference's per-instance timing, timing.h:79-82) are
 reported as `one_at_a_time`, and `latency_ms_per_reduction` is one matrix's
 stage 1 + stage 2 under overlap.  After every timed region the library's
@@ -87,19 +89,11 @@ def parse():
     p.add_argument("--one-at-a-time", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: also time K steps without the overlap (reported as one_at_a_time)")
     p.add_argument("--lanes", type=int, default=None,
-                   help="pipelined: independent stage-1/stage-2 stream pairs, matrix j on lane j mod L "
-                        "(default 8; across GPUs each lane has its own RCCL communicator)")
+                   help="pipelined: stage-1 streams, matrix j on lane j mod L (default: one GPU plan_lanes(K), "
+                        "10 for K = 20; across GPUs 8, each lane with its own RCCL communicator)")
     p.add_argument("--s2-lanes", type=int, default=None,
                    help="pipelined, one GPU: stage-2 streams (matrix j's stage 2 on stream j mod S2L; "
                         "default: one per lane)")
-    p.add_argument("--s2-priority", choices=["normal", "high"], default="normal",
-                   help="pipelined: HIP priority of the stage-2 streams")
-    p.add_argument("--drain", choices=["on", "off"], default="on",
-                   help="pipelined, one GPU: the last round's stage 2s (the drain, no stage 1 left to run) "
-                        "each on a stream of its own once every earlier stage 2 is done, the CUs split "
-                        "evenly among them (at most the usual reservation each)")
-    p.add_argument("--s1-high", type=int, default=0,
-                   help="pipelined: the first S1H stage-1 streams at high HIP priority (A/B)")
     p.add_argument("--pad", type=int, default=0,
                    help="leading dimension n + PAD elements for the device matrices")
     p.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -466,7 +460,7 @@ def main():
         # too -- all 32 -- was measured slower at world size 1, N = 8192:
         # 11.95 vs 15.30 TFLOP/s distributed and 16.9 vs 21.1 single-GPU in
         # the same process, profiles/r04_hwq_ab.txt)
-        want = min(32, args.lanes + args.s2_lanes + 4 + (args.lanes if (args.drain == "on" and not multi) else 0))
+        want = min(32, args.lanes + args.s2_lanes + 4)
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
@@ -536,8 +530,8 @@ def main():
     # world size 1 over RCCL (--force-dist, 12 steps), 14.6 vs 16.0 -- across
     # GPUs a matrix's stage 1 is a chain of per-panel collectives and factors,
     # so more matrices in flight hide more of it.
-    sa_l = [torch.cuda.Stream(dev, priority=-1 if l < args.s1_high else 0) for l in range(lanes)]
-    sb_l = [torch.cuda.Stream(dev, priority=-1 if args.s2_priority == "high" else 0) for _ in range(s2_lanes)]
+    sa_l = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    sb_l = [torch.cuda.Stream(dev) for _ in range(s2_lanes)]
     if dist_mode:
         from svdsolver_amd import dist as D
         for s_a in sa_l:   # one communicator per lane's stage-1 stream
@@ -599,15 +593,6 @@ def main():
                 S.band2bd(A, b, sigma=args.s2 == "sigma", sync=False, extract=False)
     del base
 
-    # The drain (one GPU, pipelined): once the last round's stage 1s are
-    # issued no stage-1 work is left to share the chip with, so each of the
-    # last `lanes` matrices' stage 2 gets a stream of its own (after every
-    # earlier stage 2, so at most `lanes` sweep grids are resident) and an
-    # equal share of the CUs (min(s2_cus, CUs / lanes) workgroups) instead of
-    # queueing two deep behind the s2_lanes streams.
-    dev_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    use_drain = args.drain == "on" and pipelined and not dist_mode and args.stages == "12" and s2_lanes < lanes
-    sd_l = [torch.cuda.Stream(dev) for _ in range(lanes)] if use_drain else []
 
     def issue(first, count, ev=None):
         last = None
@@ -616,23 +601,10 @@ def main():
         # parked on barriers slow the dispatch of the active one (measured:
         # stage 1 137 ms vs 89 ms with 4 lanes' streams waiting).
         nl = lanes if mode["pipe"] else 1
-        nd = min(lanes, count) if (use_drain and mode["pipe"]) else 0
-        drain_cus = max(1, min(s2_cus, dev_cus // max(nd, 1)))
-        before = []   # events: every stage 2 issued before the drain
         for i in range(count):
             j = first + i
             A = mats[j]
             s_a, s_b = sa_l[j % nl], sb_l[j % (s2_lanes if mode["pipe"] else 1)]
-            drain = i >= count - nd
-            if drain:
-                if not before:
-                    for q in sb_l:
-                        e_ = torch.cuda.Event()
-                        e_.record(q)
-                        before.append(e_)
-                s_b = sd_l[i - (count - nd)]
-                for e_ in before:
-                    s_b.wait_event(e_)
             with torch.cuda.stream(s_a):
                 if not mode["pipe"] and last is not None:
                     s_a.wait_event(last)
@@ -645,11 +617,7 @@ def main():
                 s_b.wait_event(e1)
                 if ev:
                     ev[i][1].record(s_b)
-                if drain:
-                    S.set_overlap(drain_cus)
                 stage2(A, j)
-                if drain:
-                    S.set_overlap(s2_cus)
                 last = torch.cuda.Event(enable_timing=bool(ev))
                 last.record(s_b)
                 if ev:
@@ -757,8 +725,9 @@ def main():
                                        f"{world}, whose stage 2 runs beside the following matrices' stage 1; fill "
                                        "and drain inside the timed region" if dist_mode else
                                        f"stream throughput: K independent matrices issued back to back on {lanes} "
-                                       "lane(s) of HIP streams (matrix j on lane j mod lanes; per lane stage 2 of "
-                                       "matrix i beside stage 1 of the next), fill and drain inside the timed region; "
+                                       f"stage-1 stream(s) (matrix j on lane j mod {lanes}) and {s2_lanes} stage-2 "
+                                       f"stream(s) (matrix j's stage 2 on stream j mod {s2_lanes}, after its stage 1, "
+                                       "beside the following matrices' stage 1), fill and drain inside the timed region; "
                                        "per-reduction latency under overlap: latency_ms_per_reduction; one reduction "
                                        "at a time: one_at_a_time") if pipelined else "one reduction at a time"),
                        "n": n, "band": b,
@@ -771,9 +740,6 @@ def main():
                        "pipeline": ("stage 2 of matrix i on a second HIP stream beside stage 1 of matrix i+1"
                                     if pipelined else "off: one reduction at a time"),
                        "stage2_cus": s2_cus or "all", "lanes": lanes, "stage2_streams": s2_lanes,
-                       "drain": ("the last round's stage 2s on streams of their own, the CUs split among them"
-                                 if use_drain else "off"),
-                       "stage2_priority": args.s2_priority,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},
             "latency_ms_per_reduction": round(s1 + s2, 3),

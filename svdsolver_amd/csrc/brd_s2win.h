@@ -1,6 +1,6 @@
 // Stage-2 windows on the LDS ring, b = 32, fast arithmetic (the bundle
 // kernel's hot path; included by brd_stage2.hip after rsq_nr / rcp_nr /
-// fast_mod / dpp_mov).
+// fast_mod).
 //
 // Reference: band_rd_right (svd_parallel.h:600) and band_rd_left (:617) --
 // a Householder reflector formed from the window's first row (right window)
@@ -9,14 +9,11 @@
 // Ring: band row r lives in slot r mod R; element (r, c) at
 // d[slot(r) * P + 31 + c - r] (diagonals -31 .. 2b - 1 = 63 of row r).
 //
-// W = 1: one wave per window.  Right window: lane q holds row i1 + q (32
-// elements, registers); left window: lane q holds column i1 + q.  Every lane
-// reads the source vector as an LDS broadcast and forms the reflector's
-// scalars itself, so the window is straight-line code: loads, two 32-term
-// sums (the source's squared norm and a_q . x), the scalars, the rank-1
-// update, stores.
-// W = 2: the window's rows (right) / columns (left) split over a wave pair,
-// two lanes per row / column (16 elements each), pair sums by DPP.
+// One wave per window.  Right window: lane q holds row i1 + q (32 elements,
+// registers); left window: lane q holds column i1 + q.  Every lane reads the
+// source vector as an LDS broadcast and forms the reflector's scalars itself,
+// so the window is straight-line code: loads, two 32-term sums (the source's
+// squared norm and a_q . x), the scalars, the rank-1 update, stores.
 #pragma once
 
 namespace brd {
@@ -177,131 +174,6 @@ __device__ __forceinline__ void s2_fixup1(T &a31, T &x31, const S2Fix<T> &f, T c
     x31 = p;
 }
 
-#ifndef BRD_S2_E31FIRST
-#define BRD_S2_E31FIRST 0   // 1: element 31 loaded and fixed before the window's bulk (A/B)
-#endif
-#if BRD_S2_E31FIRST
-// Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
-// j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
-// reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
-// nc = 32 (no predicates).  Element 31 (the deferred column of a fixup) is
-// loaded first and fixed before the bulk is used.
-template <typename T, bool FULL, bool LAG2>
-__device__ __forceinline__ void s2_right_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
-                                            bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
-                                            const S2Pub &pub) {
-    constexpr int N = 32;
-    const bool rok = FULL || lane < nr;
-    const T *px = rg.row(i1) + j1;
-    T *pa = rg.row(i1 + (rok ? lane : 0)) + j1;
-    const bool c31 = FULL || N - 1 < nc;
-    T x31 = c31 ? px[N - 1] : (T)0;
-    T a31 = (c31 && rok) ? pa[N - 1] : (T)0;
-    const T corner = LAG2 ? rg.row(i1 + 31)[j1 + 31] : (T)0;   // (loads without branches: see s2_pin)
-    if (LAG2) fo.xl = px[lane & 31];
-    T a[N], x[N];
-#pragma unroll
-    for (int j = 0; j < N - 1; ++j) {
-        const bool cok = FULL || j < nc;
-        x[j] = cok ? px[j] : (T)0;
-        a[j] = (cok && rok) ? pa[j] : (T)0;
-    }
-    if (LAG2 && fix) {   // the deferred column j1 + 31 of rows i1 .. i1 + 31
-        s2_fixup1<T>(a31, x31, fi, corner, lane);
-        if (lane < 32) pa[N - 1] = a31;
-        pub.publish(lane);
-    }
-    x[N - 1] = x31;
-    a[N - 1] = a31;
-    S2Sums<T> u = s2_sums<T, N>(a, x);
-    s2_pin(u);
-    const T sigp = s2_apply<T, N>(a, x, u, fo);
-    if (LAG2 && defer) {
-        fo.sig = s2_readlane(sigp, 63);
-        if ((lane & 31) == 31) fo.xl = x[N - 1];   // (the fixup above may have changed it)
-    }
-    if (rok && !(LAG2 && defer && lane == 63)) {
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (FULL || j < nc) pa[j] = a[j];
-    }
-}
-
-// Left window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior 32 x 64 at
-// j1 = i1); the reflector comes from column j1.  Lane q holds column j1 + q.
-// Rows that do not wrap the ring sit P - 1 elements apart: one base address
-// and immediate offsets.
-template <typename T, bool FULL, bool LAG2>
-__device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, int nr, int nc, int lane,
-                                           bool fix, const S2Fix<T> &fi, bool defer, S2Fix<T> &fo,
-                                           const S2Pub &pub) {
-    constexpr int N = 32;
-    const bool cok = FULL || lane < nc;
-    const int q = cok ? lane : 0;
-    const int s0 = rg.slot(i1);
-    const bool r31 = FULL || N - 1 < nr;
-    T a[N], x[N];
-    if (LAG2) fo.xl = rg.row(i1 + (lane & 31))[j1];
-    auto finish = [&](T *e31, T corner, T x31, T a31, auto store) {
-        if (LAG2 && fix) {   // the deferred row i1 + 31 of columns j1 .. j1 + 31
-            s2_fixup1<T>(a31, x31, fi, corner, lane);
-            if (lane < 32) *e31 = a31;
-            pub.publish(lane);
-        }
-        x[N - 1] = x31;
-        a[N - 1] = a31;
-        S2Sums<T> u = s2_sums<T, N>(a, x);
-        s2_pin(u);
-        const T sigp = s2_apply<T, N>(a, x, u, fo);
-        if (LAG2 && defer) {
-            fo.sig = s2_readlane(sigp, 63);
-            if ((lane & 31) == 31) fo.xl = x[N - 1];
-        }
-        if (cok && !(LAG2 && defer && lane == 63)) store();
-    };
-    if (s0 + N <= rg.R) {
-        T *bx = rg.d + s0 * rg.P + 31 + (j1 - i1);   // element (i1 + j, j1) at bx[j (P - 1)]
-        T *b31 = bx + (N - 1) * (rg.P - 1);
-        const T x31 = r31 ? b31[0] : (T)0;
-        const T a31 = (r31 && cok) ? b31[q] : (T)0;
-        const T corner = LAG2 ? b31[31] : (T)0;
-#pragma unroll
-        for (int j = 0; j < N - 1; ++j) {
-            const bool rk = FULL || j < nr;
-            x[j] = rk ? bx[j * (rg.P - 1)] : (T)0;
-            a[j] = (rk && cok) ? bx[j * (rg.P - 1) + q] : (T)0;
-        }
-        finish(b31 + q, corner, x31, a31, [&]() {
-#pragma unroll
-            for (int j = 0; j < N; ++j)
-                if (FULL || j < nr) bx[j * (rg.P - 1) + q] = a[j];
-        });
-    } else {
-        T *rows[N];
-        int s = s0;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            rows[j] = rg.d + s * rg.P + 31 + (j1 - i1) - j;
-            s = s + 1 == rg.R ? 0 : s + 1;
-        }
-        const T x31 = r31 ? rows[N - 1][0] : (T)0;
-        const T a31 = (r31 && cok) ? rows[N - 1][q] : (T)0;
-        const T corner = LAG2 ? rows[N - 1][31] : (T)0;
-#pragma unroll
-        for (int j = 0; j < N - 1; ++j) {
-            const bool rk = FULL || j < nr;
-            x[j] = rk ? rows[j][0] : (T)0;
-            a[j] = (rk && cok) ? rows[j][q] : (T)0;
-        }
-        finish(rows[N - 1] + q, corner, x31, a31, [&]() {
-#pragma unroll
-            for (int j = 0; j < N; ++j)
-                if (FULL || j < nr) rows[j][q] = a[j];
-        });
-    }
-}
-
-#else
 // Right window rows [i1, i1 + nr) x cols [j1, j1 + nc) (interior: 64 x 32 at
 // j1 = i1 + 32; a sweep's first window: 33 x 32 at j1 = i1 + 1); the
 // reflector comes from row i1.  Lane q holds row i1 + q.  FULL: nr = 64,
@@ -404,97 +276,5 @@ __device__ __forceinline__ void s2_left_w1(const S2Ring<T> &rg, int i1, int j1, 
     }
 }
 
-#endif
-
-// ---- wave pair (W = 2) ------------------------------------------------------
-// The pair's waves meet on the source vector: wave 1 raises its flag once it
-// has read the source; wave 0 (which holds the source row / column) stores
-// only after that.
-struct S2Pair {
-    int *xr;   // two flag words
-    int pw;    // 0 or 1
-    int tag;
-    __device__ __forceinline__ void read_done(int lane) const {
-        if (pw == 0) return;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(xr + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __device__ __forceinline__ void before_store() const {
-        if (pw != 0) return;
-        for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__hip_atomic_load(xr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= tag) break;
-            __builtin_amdgcn_s_sleep(0);
-        }
-    }
-};
-
-template <typename T, int N>
-__device__ __forceinline__ void s2_refl_pair(T (&a)[N], const T (&x)[N], T x0, bool piv) {
-    T q0 = (T)0, q1 = (T)0, g0 = (T)0, g1 = (T)0;
-#pragma unroll
-    for (int k = 0; k < N; k += 2) {
-        q0 = fma(x[k], x[k], q0);
-        q1 = fma(x[k + 1], x[k + 1], q1);
-        if (k > 0 || !piv) g0 = fma(a[k], x[k], g0);
-        g1 = fma(a[k + 1], x[k + 1], g1);
-    }
-    const T qq = group_sum<2>(q0 + q1);
-    const T rn = rsq_nr(qq);
-    const T nrm = qq * rn;
-    const T sgn = x0 >= (T)0 ? (T)-1 : (T)1;
-    const T u1 = fma(-sgn, nrm, x0);
-    const T alpha = rcp_nr(u1);
-    const T tau = -sgn * u1 * rn;
-    const T dot = group_sum<2>(fma(alpha, g0 + g1, piv ? a[0] : (T)0));
-    const T td = tau * dot;
-    const T tda = td * alpha;
-    const T e0 = piv ? a[0] - td : fma(-tda, x[0], a[0]);
-#pragma unroll
-    for (int k = 1; k < N; ++k) a[k] = fma(-tda, x[k], a[k]);
-    a[0] = e0;
-}
-
-// right window, interior only (64 x 32): lane L = 64 pw + lane -> row L / 2,
-// elements 16 (L % 2) + [0, 16)
-template <typename T, bool FULL>
-__device__ __forceinline__ void s2_right_w2(const S2Ring<T> &rg, int i1, int nr, int nc, int lane, const S2Pair &pr) {
-    constexpr int E = 16;
-    const int L = 64 * pr.pw + lane, h = L & 1, r = L >> 1;
-    const T *px = rg.row(i1) + i1 + 32 + E * h;
-    T *pa = rg.row(i1 + r) + i1 + 32 + E * h;
-    T a[E], x[E];
-#pragma unroll
-    for (int k = 0; k < E; ++k) { x[k] = px[k]; a[k] = pa[k]; }
-    const T x0 = rg.row(i1)[i1 + 32];
-    pr.read_done(lane);
-    s2_refl_pair<T, E>(a, x, x0, h == 0);
-    pr.before_store();
-#pragma unroll
-    for (int k = 0; k < E; ++k) pa[k] = a[k];
-}
-
-// left window, interior only (32 x 64): lane L -> column L / 2, rows 16 (L % 2) + [0, 16)
-template <typename T, bool FULL>
-__device__ __forceinline__ void s2_left_w2(const S2Ring<T> &rg, int i1, int nr, int nc, int lane, const S2Pair &pr) {
-    constexpr int E = 16;
-    const int L = 64 * pr.pw + lane, h = L & 1, c = L >> 1;
-    const int s0 = rg.slot(i1 + E * h);
-    T a[E], x[E];
-    T *rows[E];
-    int s = s0;
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        rows[k] = rg.d + s * rg.P + 31 - (E * h + k);
-        s = s + 1 == rg.R ? 0 : s + 1;
-        x[k] = rows[k][0];
-        a[k] = rows[k][c];
-    }
-    const T x0 = rg.row(i1)[i1];
-    pr.read_done(lane);
-    s2_refl_pair<T, E>(a, x, x0, h == 0);
-    pr.before_store();
-#pragma unroll
-    for (int k = 0; k < E; ++k) rows[k][c] = a[k];
-}
 
 }  // namespace brd

@@ -17,112 +17,20 @@
 //                is bit-identical to the reference's CPU code on the same
 //                input (used to pin the geometry in tests).
 //
-// Two schedules (DESIGN.md "Stage 2"):
-//   k_band2bd_bundle  (default) bundles of S consecutive sweeps per workgroup,
-//                     one wave per sweep, the active band rows in an LDS ring
-//                     filled / drained by an IO wave; bundles hand rows to the
-//                     next bundle through HBM.
-//   k_band2bd_pipe    one wave per sweep straight on HBM (sc1 hand-offs).
+// Three kernels (DESIGN.md "Stage 2"):
+//   k_sweeps          fast mode, b = 32 (production): bundles of S sweeps per
+//                     workgroup on an LDS ring, one straight-line wave per
+//                     window (brd_s2win.h), loader / writer / poller waves.
+//   k_band2bd_bundle  exact order, and fast mode for b != 32: the same bundle
+//                     scheme with the generic (predicated) one-wave windows.
+//   k_band2bd_pipe    bands too small for a ring (n < 64): one wave per sweep
+//                     straight on HBM (sc1 hand-offs).
 #include "brd_internal.h"
 
 #include <algorithm>
 #include <cstdlib>
 
 namespace brd {
-
-#ifdef BRD_STAMPS
-// Debug build only: per-bundle timeline (s_memtime) of k_band2bd_bundle:
-// [0] bundle start, [1] leading sweep task 0 done, [2] leading sweep done,
-// [3] trailing sweep done, [4] writer done, [5] loader done.
-constexpr int kS2Stamp = 6, kS2MaxBundles = 4096;
-__device__ unsigned long long g_s2stamps[kS2MaxBundles * kS2Stamp];
-#define S2STAMP(beta, k)                                                         \
-    do {                                                                         \
-        if ((beta) < kS2MaxBundles) g_s2stamps[(beta) * kS2Stamp + (k)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-// Per-bundle cycle accounting, kept in registers and stored once per bundle
-// (a global update inside the loop would sit in the loader's vmcnt queue):
-// slots [4 * wave + j]: compute waves {0: wait prev sweep, 1: wait rows, 2: work},
-// loader {0: issue / poll, 1: wait landed}, writer {0: wait rows, 1: write}.
-constexpr int kS2Acc = 32;
-__device__ unsigned long long g_s2acc[kS2MaxBundles * kS2Acc];
-// Cross-CU event times (s_memrealtime, 100 MHz, one clock for the whole chip)
-// for the hand-off of row X(beta) = beta*S + 300 from bundle beta to beta+1:
-// [beta][0] trail of beta moves its front past X, [beta][1] beta's writer
-// publishes rows_done > X, [beta+1][2] beta+1's poller sees it, [beta+1][3]
-// beta+1's loader publishes loaded > X, [beta+1][4] beta+1's lead starts the
-// first window that reaches row X.
-constexpr int kS2Ev = 8;
-__device__ unsigned long long g_s2ev[kS2MaxBundles * kS2Ev];
-hipError_t read_s2ev(unsigned long long *out, size_t n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2ev), sizeof(unsigned long long) * n);
-}
-#define S2EV(beta, k, cond)                                                                  \
-    do {                                                                                     \
-        if (!s2e[k] && (cond)) {                                                             \
-            s2e[k] = true;                                                                   \
-            if ((beta) < kS2MaxBundles) g_s2ev[(beta) * kS2Ev + (k)] = __builtin_amdgcn_s_memrealtime(); \
-        }                                                                                    \
-    } while (0)
-// Per-task timeline of bundles kTB0 and kTB0+1 (s_memrealtime): per compute
-// wave and task {start, ready (waits done), end}; and every publish of
-// {loaded, rows_done, avail} as (time, value).
-constexpr int kTB0 = 1000, kTT = 520, kPub = 2048;
-__device__ unsigned long long g_tt[2][4][kTT][3];
-__device__ unsigned long long g_pub[2][3][kPub][2];
-__device__ int g_npub[2][3];
-hipError_t reset_s2tt() {
-    static int z[2][3] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_npub), z, sizeof(z));
-}
-hipError_t read_s2tt(void *tt, void *pub, void *npub) {
-    hipError_t e = hipMemcpyFromSymbol(tt, HIP_SYMBOL(g_tt), sizeof(g_tt));
-    if (e == hipSuccess) e = hipMemcpyFromSymbol(pub, HIP_SYMBOL(g_pub), sizeof(g_pub));
-    if (e == hipSuccess) e = hipMemcpyFromSymbol(npub, HIP_SYMBOL(g_npub), sizeof(g_npub));
-    return e;
-}
-#define S2TT(beta, w, t, k)                                                                     \
-    do {                                                                                        \
-        if ((beta) >= kTB0 && (beta) < kTB0 + 2 && (t) < kTT && lane == 0)                      \
-            g_tt[(beta) - kTB0][w][t][k] = __builtin_amdgcn_s_memrealtime();                     \
-    } while (0)
-#define S2PUB(beta, kind, val)                                                                  \
-    do {                                                                                        \
-        if ((beta) >= kTB0 && (beta) < kTB0 + 2 && lane == 0) {                                  \
-            const int q_ = g_npub[(beta) - kTB0][kind]++;                                       \
-            if (q_ < kPub) {                                                                    \
-                g_pub[(beta) - kTB0][kind][q_][0] = __builtin_amdgcn_s_memrealtime();           \
-                g_pub[(beta) - kTB0][kind][q_][1] = (val);                                      \
-            }                                                                                   \
-        }                                                                                       \
-    } while (0)
-hipError_t read_s2stamps(unsigned long long *out, size_t n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2stamps), sizeof(unsigned long long) * n);
-}
-hipError_t read_s2acc(unsigned long long *out, size_t n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2acc), sizeof(unsigned long long) * n);
-}
-#define S2T0() const unsigned long long _t0 = __builtin_amdgcn_s_memtime()
-#define S2T(var) var = __builtin_amdgcn_s_memtime()
-#define S2ACC(beta, k, t0, t1) do { s2a[k] += (t1) - (t0); } while (0)
-#define S2FLUSH(beta)                                                                  \
-    do {                                                                               \
-        if ((beta) < kS2MaxBundles && lane == 0)                                       \
-            for (int j_ = 0; j_ < 4; ++j_) g_s2acc[(beta) * kS2Acc + 4 * wave + j_] += s2a[j_]; \
-    } while (0)
-#else
-#define S2STAMP(beta, k) do {} while (0)
-#define S2EV(beta, k, cond) do {} while (0)
-#define S2TT(beta, w, t, k) do {} while (0)
-#define S2PUB(beta, kind, val) do {} while (0)
-#define S2ACC(beta, k, t0, t1) do {} while (0)
-#define S2FLUSH(beta) do {} while (0)
-#endif
-#ifdef BRD_STAMPS
-#define S2CLK() __builtin_amdgcn_s_memtime()
-#else
-#define S2CLK() 0ull
-#endif
 
 template <typename T>
 __device__ __forceinline__ T ld_c(const T *p) {
@@ -335,135 +243,6 @@ __device__ void win_left(const Acc &A, int i1, int i2, int j1, int j2, WaveLds<T
     }
 }
 
-// ---- full interior windows in the LDS ring, fast mode, compile-time B ------
-// Away from the matrix edge every right window is 2B x B and every left window
-// B x 2B (B = b).  These paths carry no per-element predicates: every lane
-// reads the reflector source x as an LDS broadcast and forms alpha and tau
-// itself (no serial lane-0 section), and w_c = alpha x_c is folded into the
-// dot product and the update:
-//   sigma = sum_{c>=1} a_c x_c,  dot = a_0 + alpha sigma,  a_0 -= tau dot,
-//   a_c -= (tau dot alpha) x_c.
-template <typename T, int N>
-__device__ __forceinline__ void refl_scalars(const T (&x)[N], T &alpha, T &tau) {
-    T q0 = (T)0, q1 = (T)0, q2 = (T)0, q3 = (T)0;
-#pragma unroll
-    for (int r = 0; r < N; r += 4) {
-        q0 = fma(x[r], x[r], q0);
-        if (r + 1 < N) q1 = fma(x[r + 1], x[r + 1], q1);
-        if (r + 2 < N) q2 = fma(x[r + 2], x[r + 2], q2);
-        if (r + 3 < N) q3 = fma(x[r + 3], x[r + 3], q3);
-    }
-    const T nrm = sqrt((q0 + q1) + (q2 + q3));
-    const double s = x[0] >= (T)0 ? -1.0 : 1.0;
-    const double u1 = (double)x[0] - s * (double)nrm;
-    alpha = (T)(1. / u1);
-    tau = (T)(-s * u1 / (double)nrm);
-}
-
-template <typename T, int N>
-__device__ __forceinline__ void refl_update(T (&a)[N], const T (&x)[N], T alpha, T tau) {
-    T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
-#pragma unroll
-    for (int c = 1; c < N; c += 4) {
-        s0 = fma(a[c], x[c], s0);
-        if (c + 1 < N) s1 = fma(a[c + 1], x[c + 1], s1);
-        if (c + 2 < N) s2 = fma(a[c + 2], x[c + 2], s2);
-        if (c + 3 < N) s3 = fma(a[c + 3], x[c + 3], s3);
-    }
-    const T dot = fma(alpha, (s0 + s1) + (s2 + s3), a[0]);
-    const T td = tau * dot;
-    a[0] -= td;
-    const T tda = td * alpha;
-#pragma unroll
-    for (int c = 1; c < N; ++c) a[c] = fma(-tda, x[c], a[c]);
-}
-
-// right window rows [i1, i1+2B) x cols [j1, j1+B); lane = row - i1 (lanes >= 2B idle)
-template <typename T, int B>
-__device__ __forceinline__ void win_right_full(const RingAcc<T> &A, int i1, int j1, int lane) {
-    const int r = i1 + (lane < 2 * B ? lane : 0);
-    const T *px = A.row(i1) + j1;
-    T *pa = A.row(r) + j1;
-    T a[B], x[B];
-#pragma unroll
-    for (int c = 0; c < B; ++c) { x[c] = px[c]; a[c] = pa[c]; }
-    T alpha, tau;
-    refl_scalars<T, B>(x, alpha, tau);
-    refl_update<T, B>(a, x, alpha, tau);
-    if (lane < 2 * B) {
-#pragma unroll
-        for (int c = 0; c < B; ++c) pa[c] = a[c];
-    }
-}
-
-// left window rows [i1, i1+B) x cols [j1, j1+2B); lane = col - j1 (lanes >= 2B idle)
-template <typename T, int B>
-__device__ __forceinline__ void win_left_full(const RingAcc<T> &A, int i1, int j1, int lane) {
-    const int col = lane < 2 * B ? lane : 0;
-    int slot = A.slot(i1);
-    T a[B], x[B];
-    T *rows[B];
-#pragma unroll
-    for (int r = 0; r < B; ++r) {
-        rows[r] = A.d + slot * A.P + A.off - (i1 + r) + j1;
-        x[r] = rows[r][0];
-        a[r] = rows[r][col];
-        slot = slot + 1 == A.R ? 0 : slot + 1;
-    }
-    T alpha, tau;
-    refl_scalars<T, B>(x, alpha, tau);
-    refl_update<T, B>(a, x, alpha, tau);
-    if (lane < 2 * B) {
-#pragma unroll
-        for (int r = 0; r < B; ++r) rows[r][col] = a[r];
-    }
-}
-
-// ---- full interior windows split over W waves (fast mode, B = 32) -----------
-// A window's rows (right window) or columns (left window) get W lanes each,
-// every lane holding E = B / W consecutive elements of its row / column, so
-// the per-lane work of a window -- its latency on the stage-2 critical path --
-// drops by W.  The W lanes of a row / column are consecutive lanes of one
-// quad, so partial norms and dot products are combined by DPP (xor 1, xor 2)
-// without LDS.  Every lane forms the reflector's scalars itself (hardware
-// rsq / rcp refined by Newton steps).  Lane layout (L = 64 pw + lane, pw =
-// the wave's index within the sweep):
-//   right window rows [i1, i1+2B) x cols [j1, j1+B): row L / W, columns (L % W) E + [0, E)
-//   left window  rows [i1, i1+B) x cols [j1, j1+2B): column L / W, rows (L % W) E + [0, E)
-// Both are LDS-bank-conflict-free: element (r, c) of the ring sits at
-// dword 2 ((c - r) mod 32) modulo 64 (pitch 3b rounded to 16 B), and the 32
-// lanes of a half-wave touch 32 distinct c - r.
-// The source row / column (element group 0) belongs to wave pw = 0, which
-// must not store before the other waves have read it: they raise their
-// x-flag (tag) once their loads have returned, and wave 0 checks all flags
-// before its stores (MultiSync).
-template <typename T, int CTRL>
-__device__ __forceinline__ T dpp_mov(T v);
-template <>
-__device__ __forceinline__ double dpp_mov<double, 0xB1>(double v) {
-    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0xB1, 0xf, 0xf, false),
-                            __builtin_amdgcn_update_dpp(0, __double2loint(v), 0xB1, 0xf, 0xf, false));
-}
-template <>
-__device__ __forceinline__ double dpp_mov<double, 0x4E>(double v) {
-    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x4E, 0xf, 0xf, false),
-                            __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x4E, 0xf, 0xf, false));
-}
-template <>
-__device__ __forceinline__ float dpp_mov<float, 0xB1>(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));
-}
-template <>
-__device__ __forceinline__ float dpp_mov<float, 0x4E>(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));
-}
-// sum over the W consecutive lanes of a group (W = 1, 2, 4)
-template <int W, typename T>
-__device__ __forceinline__ T group_sum(T v) {
-    if constexpr (W >= 2) v += dpp_mov<T, 0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
-    if constexpr (W >= 4) v += dpp_mov<T, 0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
-    return v;
-}
 // 1/sqrt(q) and 1/u: hardware estimate refined by Newton steps to full precision
 // The hardware estimates flush denormal inputs and results, so arguments
 // near the ends of the exponent range are rescaled by a power of two first
@@ -500,107 +279,6 @@ __device__ __forceinline__ float rcp_nr(float u) {
     const float us = u * sc;
     const float y = __builtin_amdgcn_rcpf(us);
     return fmaf(y, fmaf(-us, y, 1.0f), y) * sc;
-}
-// Apply the reflector of the source vector x (x0 = its element 0, the pivot)
-// to a; this lane holds elements [q E, q E + E) of both.
-template <typename T, int E, int W>
-__device__ __forceinline__ void refl_apply_multi(T (&a)[E], const T (&x)[E], T x0, int q) {
-    T s2[4] = {(T)0, (T)0, (T)0, (T)0}, sg[4] = {(T)0, (T)0, (T)0, (T)0};
-#pragma unroll
-    for (int k = 0; k < E; ++k) s2[k & 3] = fma(x[k], x[k], s2[k & 3]);
-#pragma unroll
-    for (int k = 1; k < E; ++k) sg[k & 3] = fma(a[k], x[k], sg[k & 3]);
-    const bool piv = q == 0;                       // this lane holds element 0
-    if (!piv) sg[0] = fma(a[0], x[0], sg[0]);
-    const T qq = group_sum<W>((s2[0] + s2[1]) + (s2[2] + s2[3]));
-    const T sig = (sg[0] + sg[1]) + (sg[2] + sg[3]);
-    const T rn = rsq_nr(qq);
-    const T nrm = qq * rn;
-    const T sgn = x0 >= (T)0 ? (T)-1 : (T)1;
-    const T u1 = fma(-sgn, nrm, x0);
-    const T alpha = rcp_nr(u1);
-    const T tau = -sgn * u1 * rn;
-    const T dot = group_sum<W>(fma(alpha, sig, piv ? a[0] : (T)0));   // w^T a, w_0 = 1, w_c = alpha x_c
-    const T td = tau * dot;
-    const T tda = td * alpha;
-    const T e0 = piv ? a[0] - td : fma(-tda, x[0], a[0]);
-#pragma unroll
-    for (int k = 1; k < E; ++k) a[k] = fma(-tda, x[k], a[k]);
-    a[0] = e0;
-}
-
-struct MultiSync {
-    int *xr;      // x-flags of the sweep's W waves
-    int pw, W, tag;
-    __device__ __forceinline__ void read_done(int lane) const {
-        if (pw == 0) return;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(xr + pw, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __device__ __forceinline__ void before_store() const {
-        if (pw != 0) return;
-        for (int w = 1; w < W; ++w)
-            while (__hip_atomic_load(xr + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tag)
-                __builtin_amdgcn_s_sleep(0);
-    }
-};
-
-// FULL = false: an edge window clipped to rows [i1, i2), cols [j1, j2) (right:
-// at most 2B x B, left: at most B x 2B); lanes and elements outside it hold
-// zeros, which leave the reflector and the dot products unchanged.
-template <typename T, int B, int W, bool FULL>
-__device__ __forceinline__ void win_right_multi(const RingAcc<T> &A, int i1, int i2, int j1, int j2, int L,
-                                                int lane, const MultiSync &ms) {
-    constexpr int E = B / W;
-    const int q = L % W, r = L / W;
-    const bool rok = FULL || i1 + r < i2;
-    const T *px = A.row(i1) + j1;
-    T *pa = A.row(i1 + (rok ? r : 0)) + j1 + q * E;
-    T a[E], x[E];
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        const bool cok = FULL || j1 + q * E + k < j2;
-        x[k] = cok ? px[q * E + k] : (T)0;
-        a[k] = (cok && rok) ? pa[k] : (T)0;
-    }
-    const T x0 = px[0];
-    ms.read_done(lane);
-    refl_apply_multi<T, E, W>(a, x, x0, q);
-    ms.before_store();
-    if (rok) {
-#pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (FULL || j1 + q * E + k < j2) pa[k] = a[k];
-    }
-}
-
-template <typename T, int B, int W, bool FULL>
-__device__ __forceinline__ void win_left_multi(const RingAcc<T> &A, int i1, int i2, int j1, int j2, int L,
-                                               int lane, const MultiSync &ms) {
-    constexpr int E = B / W;
-    const int q = L % W, c = L / W;
-    const bool cok = FULL || j1 + c < j2;
-    const int col = cok ? c : 0;
-    int slot = A.slot(i1 + q * E);
-    T a[E], x[E];
-    T *rows[E];
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        const bool rk = FULL || i1 + q * E + k < i2;
-        rows[k] = A.d + slot * A.P + A.off - (i1 + q * E + k) + j1;
-        x[k] = rk ? rows[k][0] : (T)0;
-        a[k] = (rk && cok) ? rows[k][col] : (T)0;
-        slot = slot + 1 == A.R ? 0 : slot + 1;
-    }
-    const T x0 = A.row(i1)[j1];
-    ms.read_done(lane);
-    refl_apply_multi<T, E, W>(a, x, x0, q);
-    ms.before_store();
-    if (cok) {
-#pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (FULL || i1 + q * E + k < i2) rows[k][col] = a[k];
-    }
 }
 
 // ---- the reference's task list of one sweep --------------------------------
@@ -757,7 +435,6 @@ struct BundleFlags {
     int loaded;      // rows < loaded are in the ring (loader wave)
     int freed;       // ring slots of rows < freed may be reused (writer wave)
     int avail;       // rows < avail have been written back by bundle beta-1 (poller wave)
-    int xr[16];      // wave pairs: the task (+1) whose reflector source this wave has read
 };
 
 __device__ __forceinline__ int lds_acq(const int *p) {
@@ -767,25 +444,10 @@ __device__ __forceinline__ void lds_rel(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Workgroup = S compute waves + loader + writer + poller.  fp64 bundles are
-// LDS-limited to S = 2 (the ring also needs slack for the loader, see
-// bundle_plan); fp32 to S = 5 (512 threads).
-// W = compute waves per sweep: 2 on the b = 32 fast path (windows split over a
-// wave pair), else 1.
-// Threads of a bundle workgroup: W compute waves per sweep for up to 3 (fp64,
-// LDS-limited) or 5 (fp32) sweeps, plus the loader, writer and poller waves;
-// at most 1024.
-template <typename T, int W> constexpr int bundle_max_threads() {
-    return 64 * (W * (sizeof(T) == 8 ? 3 : 5) + 3) < 1024 ? 64 * (W * (sizeof(T) == 8 ? 3 : 5) + 3) : 1024;
-}
-// smallest progress count of the W waves of one sweep
-template <int W>
-__device__ __forceinline__ int prog_min(const int *p) {
-    int m = lds_acq(p);
-#pragma unroll
-    for (int w = 1; w < W; ++w) m = min(m, lds_acq(p + w));
-    return m;
-}
+// Workgroup = S compute waves (one per sweep) + loader + writer + poller:
+// up to 3 (fp64, LDS-limited: the ring also needs slack for the loader, see
+// bundle_plan) or 5 (fp32) sweeps.
+template <typename T> constexpr int bundle_max_threads() { return 64 * ((sizeof(T) == 8 ? 3 : 5) + 3); }
 // (BRD_S2_* macros: developer A/B builds, tools/variant_lib.sh; measured at
 // N = 8192 fp64, round 2: 63 rows in flight 87.3 vs 87.6 ms, 4-row loader
 // chunks 93.2, 16-row writer batches 89.0, compute waves at s_setprio 2 87.2 --
@@ -870,8 +532,8 @@ __device__ __forceinline__ void st16_sc1(void *p, u32x4 v) {
 }
 
 
-template <typename T, bool EXACT, int KB, int W>
-__global__ void __launch_bounds__((bundle_max_threads<T, W>()))
+template <typename T, bool EXACT>
+__global__ void __launch_bounds__((bundle_max_threads<T>()))
 k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned magic, int *rows_done, int *err)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -890,30 +552,17 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
         const int nsw = min(S, n - 1 - i0);
         if (threadIdx.x < 16) {
             F->prog[threadIdx.x] = 0;
-            F->xr[threadIdx.x] = 0;
-            F->front[threadIdx.x] = (int)threadIdx.x < W * nsw ? i0 + (int)threadIdx.x / W : n;
+            F->front[threadIdx.x] = (int)threadIdx.x < nsw ? i0 + (int)threadIdx.x : n;
         }
         if (threadIdx.x == 0) { F->loaded = i0; F->freed = i0; F->avail = 0; }
         __syncthreads();
-        if (threadIdx.x == 0) S2STAMP(beta, 0);
-#ifdef BRD_STAMPS
-        unsigned long long s2a[4] = {0, 0, 0, 0};
-        bool s2e[7] = {false, false, false, false, false, false, false};
-#endif
 
-        if (wave < W * nsw) {
-            // ---------------- compute wave(s): sweep i0 + sw ----------------
-            // W waves per sweep (waves W sw .. W sw + W - 1, pw = 0 .. W-1): full
-            // windows are split over them (win_*_multi), the others run on wave
-            // pw = 0 alone.  Before task t every wave waits for all W waves of its
-            // sweep to finish task t - 1 (a window reads what the whole previous
-            // window wrote) and, by the lag-3 rule, for all W waves of the
-            // previous sweep to finish task t + 3.
-            const int sw = wave / W, pw = wave - sw * W;
+        if (wave < nsw) {
+            // ---------------- compute wave: sweep i0 + sw ----------------
+            // Before task t the wave waits, by the lag-3 rule, for the previous
+            // sweep to finish task t + 3.
+            const int sw = wave;
             const int i = i0 + sw;
-#ifdef BRD_S2_PRIO
-            __builtin_amdgcn_s_setprio(BRD_S2_PRIO);
-#endif
             SweepIter it;
             it.init(n, n, b, i, sigma);
             const int prev_ntask = sw > 0 ? sweep_ntask(n, n, b, i - 1, sigma) : 0;
@@ -922,74 +571,27 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                 const Win wnd = it.task(t, right);
                 const bool live = wnd.j2 > wnd.j1 && wnd.i2 > wnd.i1;
                 int spins = 0;
-                unsigned long long c0 = S2CLK();
-                S2TT(beta, wave, t, 0);
                 if (sw > 0) {
                     const int need = min(t + 4, prev_ntask);
-                    while (prog_min<W>(F->prog + W * (sw - 1)) < need) {
+                    while (lds_acq(F->prog + sw - 1) < need) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 2); break; }
                     }
                 }
-                if constexpr (W > 1) {
-                    while (prog_min<W>(F->prog + W * sw) < t) {
-                        __builtin_amdgcn_s_sleep(0);
-                        if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 7); break; }
-                    }
-                }
-                unsigned long long c1 = S2CLK();
-                S2ACC(beta, 0, c0, c1);
                 if (live) {
                     while (lds_acq(&F->loaded) < wnd.i2) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > kSpinLimit) { if (lane == 0) st_c(err, 3); break; }
                     }
-                    c0 = S2CLK();
-                    S2ACC(beta, 1, c1, c0);
-                    if (lane == 0) S2EV(beta, 4, wave == 0 && wnd.i2 > (beta - 1) * S + 300);
-                    S2TT(beta, wave, t, 1);
-                    const int wr = wnd.i2 - wnd.i1, wc = wnd.j2 - wnd.j1;
-                    if constexpr (KB > 0) {
-                        const bool full_r = right && wr == 2 * KB && wc == KB;
-                        const bool full_l = !right && wr == KB && wc == 2 * KB;
-                        if constexpr (W > 1) {
-                            // every window of the sweep on all W waves: full ones
-                            // unpredicated, clipped edge windows predicated
-                            const MultiSync ms{F->xr + W * sw, pw, W, t + 1};
-                            const int L = 64 * pw + lane;
-                            if (full_r) win_right_multi<T, KB, W, true>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
-                            else if (full_l) win_left_multi<T, KB, W, true>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
-                            else if (right) win_right_multi<T, KB, W, false>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
-                            else            win_left_multi<T, KB, W, false>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, L, lane, ms);
-                        } else {
-                            if (full_r) win_right_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
-                            else if (full_l) win_left_full<T, KB>(acc, wnd.i1, wnd.j1, lane);
-                            else if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                            else            win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                        }
-                    } else {
-                        if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                        else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
-                    }
-                    c1 = S2CLK();
-                    S2ACC(beta, 2, c0, c1);
+                    if (right) win_right<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
+                    else       win_left<T, EXACT>(acc, wnd.i1, wnd.i2, wnd.j1, wnd.j2, wl[sw], lane);
                 }
-                S2TT(beta, wave, t, 2);
                 if (lane == 0) {
                     lds_rel(&F->front[wave], it.next_top(t));
                     lds_rel(&F->prog[wave], t + 1);
-                    S2EV(beta, 0, wave == W * nsw - 1 && it.next_top(t) > beta * S + 300);
-                    S2EV(beta, 5, wave == 0 && t == 0);            // lead: first task done
-                    S2EV(beta, 6, wave == 0 && t == it.ntask - 1);  // lead: sweep done
-                    if (wave == 0 && t == 0) S2STAMP(beta, 1);
                 }
             }
-#ifdef BRD_S2_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            if (lane == 0 && wave == 0) S2STAMP(beta, 2);
-            if (lane == 0 && wave == W * nsw - 1) S2STAMP(beta, 3);
-        } else if (wave == W * S) {
+        } else if (wave == S) {
             // ---------------- loader wave: HBM -> ring by LDS-DMA ----------------
             // An interior row (all P columns inside the matrix) is copied by ONE
             // global_load_lds_dwordx4 (lane q moves 16-byte piece q, sc1) straight
@@ -1012,7 +614,6 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
             const char *src = (const char *)(A + (long)i0 * lda + i0 - (b - 1)) + 16 * lane;
             const long rstep = (lda + 1) * (long)sizeof(T);
             const bool dma_lane = lane < row_q;
-            unsigned long long c0 = S2CLK();
             while (rl < n) {
                 const int av = __hip_atomic_load(&F->avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const int fr = __hip_atomic_load(&F->freed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1049,16 +650,10 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     }
                 }
                 if (ra > rl) {
-                    unsigned long long c1 = S2CLK();
-                    S2ACC(beta, 0, c0, c1);
                     const int keep = max(0, ra - rl - kChunk);
                     wait_vmcnt(keep);
                     rl = ra - keep;
                     if (lane == 0) lds_rel(&F->loaded, rl);
-                    if (lane == 0) S2EV(beta, 3, rl > (beta - 1) * S + 300);
-                    S2PUB(beta, 0, rl);
-                    c0 = S2CLK();
-                    S2ACC(beta, 1, c1, c0);
                     spins = 0;
                 } else if (!moved) {
                     __builtin_amdgcn_s_sleep(1);
@@ -1066,8 +661,7 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) S2STAMP(beta, 5);
-        } else if (wave == W * S + 2) {
+        } else if (wave == S + 2) {
             // ---------------- poller wave: rows bundle beta-1 has written back ----------------
             if (beta == 0) {
                 if (lane == 0) lds_rel(&F->avail, n);
@@ -1079,8 +673,6 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     if (v != av) {
                         av = v;
                         if (lane == 0) lds_rel(&F->avail, v);
-                        if (lane == 0) S2EV(beta, 2, v > (beta - 1) * S + 300);
-                        S2PUB(beta, 2, v);
                         spins = 0;
                     } else {
                         __builtin_amdgcn_s_sleep(1);
@@ -1088,7 +680,7 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     }
                 }
             }
-        } else if (wave == W * S + 1) {
+        } else if (wave == S + 1) {
             // ---------------- writer wave: ring -> HBM ----------------
             // Writes every row below all fronts (no sweep of the bundle touches it
             // again), <= kWriteRows per batch: ring -> registers (the slots are
@@ -1098,17 +690,14 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
             // so the drain of one batch overlaps the next.
             const int row_q = P * (int)sizeof(T) / 16;
             int wb = i0, spins = 0, pend = -1;
-            unsigned long long c0 = S2CLK();
             while (wb < n) {
                 int fmin = n;
-                for (int s = 0; s < W * nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
+                for (int s = 0; s < nsw; ++s) fmin = min(fmin, lds_acq(&F->front[s]));
                 const int wt = __builtin_amdgcn_readfirstlane(min(min(fmin, lds_acq(&F->loaded)), wb + kWriteRows));
                 if (wt <= wb) {
                     if (pend >= 0) {   // idle: retire the batch in flight
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         if (lane == 0) st_c(rows_done + beta, pend);
-                        if (lane == 0) S2EV(beta, 1, pend > beta * S + 300);
-                        S2PUB(beta, 1, pend);
                         pend = -1;
                         continue;
                     }
@@ -1117,8 +706,6 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     continue;
                 }
                 spins = 0;
-                unsigned long long c1 = S2CLK();
-                S2ACC(beta, 0, c0, c1);
                 const int k = wt - wb;
                 const bool interior = wb >= b - 1 && wt - 1 - (b - 1) + P <= n;
                 // the batch moves in sub-chunks of kSubRows rows (registers: one
@@ -1163,14 +750,8 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                 }
                 if (interior) {
                     if (pend >= 0) {   // everything older than this batch's k stores has drained
-                        unsigned long long c2 = S2CLK();
-                        S2ACC(beta, 2, c1, c2);
                         wait_vmcnt(k);
-                        c1 = S2CLK();
-                        S2ACC(beta, 3, c2, c1);
                         if (lane == 0) st_c(rows_done + beta, pend);
-                        if (lane == 0) S2EV(beta, 1, pend > beta * S + 300);
-                        S2PUB(beta, 1, pend);
                     }
                     pend = wt;
                 } else {
@@ -1179,16 +760,12 @@ k_band2bd_bundle(T *A, int n, long lda, int b, int sigma, int S, int R, unsigned
                     pend = -1;
                 }
                 wb = wt;
-                c0 = S2CLK();
-                S2ACC(beta, 1, c1, c0);
             }
             if (pend >= 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) st_c(rows_done + beta, pend);
             }
-            if (lane == 0) S2STAMP(beta, 4);
         }
-        S2FLUSH(beta);
         __syncthreads();
     }
 }
@@ -1731,26 +1308,11 @@ static size_t bundle_lds_bytes(int b, int S, int R) {
     return ring + (size_t)S * sizeof(WaveLds<T, EXACT>) + sizeof(BundleFlags);
 }
 
-// Compute waves per sweep on the b = 32 fast path (BRD_S2_W: 1, 2 or 4).
-// Measured at N = 8192 fp64 (3 sweeps per bundle, same box): W = 1 96.5 ms,
-// W = 2 90.9 ms, W = 4 114.5 ms -- four waves per window pay more in
-// per-task synchronisation (all W waves of a sweep meet before every task)
-// than they save in window latency.
-static int s2_waves_per_sweep() {
-    static int w = 0;
-    if (!w) {
-        const char *e = getenv("BRD_S2_W");
-        const int v = e ? atoi(e) : 2;
-        w = (v == 1 || v == 2 || v == 4) ? v : 2;
-    }
-    return w;
-}
-
-template <typename T, bool EXACT, int W>
+template <typename T, bool EXACT>
 static bool bundle_plan(int n, int b, int &S, int &R) {
     const size_t budget = 160 * 1024 - 512;
     static const char *senv = getenv("BRD_S2_SWEEPS");   // tuning: cap on sweeps per bundle
-    int smax = EXACT ? 2 : (bundle_max_threads<T, W>() / 64 - 3) / W;
+    int smax = EXACT ? 2 : bundle_max_threads<T>() / 64 - 3;
     if (senv && atoi(senv) > 0) smax = std::min(smax, atoi(senv));
     // Prefer the most sweeps whose ring keeps 16 rows of slack beyond the
     // minimum (the loader's run-ahead; more sweeps per bundle amortise the
@@ -1852,8 +1414,7 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
     const bool pipe = sel && sel[0] == 'p';
     int S = 0, R = 0;
     const bool fast32 = !exact_order && b == 32;
-    const char *legacy = getenv("BRD_S2_LEGACY");   // 1: k_band2bd_bundle for b = 32 fast too (A/B)
-    if (!pipe && fast32 && !(legacy && legacy[0] == '1') && n >= 64 && sweeps_plan<T>(n, S, R)) {
+    if (!pipe && fast32 && n >= 64 && sweeps_plan<T>(n, S, R)) {
         const int nbundles = (n - 1 + S - 1) / S;
         const dim3 block(64 * (S + 2 + kSweepWriters));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
@@ -1870,20 +1431,14 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         else     hipLaunchKernelGGL((k_sweeps<T, 16>), dim3(grid), block, lds, s, A, n, lda, sg, S, R, magic, prog, err, st);
         return hipGetLastError();
     }
-    const int W = fast32 ? s2_waves_per_sweep() : 1;
-    const bool ok = exact_order ? bundle_plan<T, true, 1>(n, b, S, R)
-                    : W == 4    ? bundle_plan<T, false, 4>(n, b, S, R)
-                    : W == 2    ? bundle_plan<T, false, 2>(n, b, S, R)
-                                : bundle_plan<T, false, 1>(n, b, S, R);
-    if (!pipe && ok && n >= 64) {   // tiny bands: the pipe schedule
+    // exact order, and fast mode for b != 32: the one-wave-per-sweep bundle
+    // kernel (k_band2bd_bundle); tiny bands: the pipe schedule
+    const bool ok = exact_order ? bundle_plan<T, true>(n, b, S, R) : bundle_plan<T, false>(n, b, S, R);
+    if (!pipe && ok && n >= 64) {
         const int nbundles = (n - 1 + S - 1) / S;
-        const dim3 block(64 * (W * S + 3));
+        const dim3 block(64 * (S + 3));
         const unsigned magic = (unsigned)((0x100000000ull + R - 1) / R);
-        const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true, 0, 1>
-                         : W == 4    ? (const void *)k_band2bd_bundle<T, false, 32, 4>
-                         : W == 2    ? (const void *)k_band2bd_bundle<T, false, 32, 2>
-                         : fast32    ? (const void *)k_band2bd_bundle<T, false, 32, 1>
-                                     : (const void *)k_band2bd_bundle<T, false, 0, 1>;
+        const void *fn = exact_order ? (const void *)k_band2bd_bundle<T, true> : (const void *)k_band2bd_bundle<T, false>;
         const size_t lds = exact_order ? bundle_lds_bytes<T, true>(b, S, R) : bundle_lds_bytes<T, false>(b, S, R);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -1891,15 +1446,9 @@ hipError_t launch_band2bd(T *A, int n, long lda, int b, bool exact_order, bool s
         if (cap < 1) return hipErrorInvalidConfiguration;
         const int grid = std::max(1, std::min(std::min(nwaves, cap), nbundles));
         if (exact_order)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, true, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
-        else if (W == 4)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 4>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
-        else if (W == 2)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 2>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
-        else if (fast32)
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 32, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, true>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         else
-            hipLaunchKernelGGL((k_band2bd_bundle<T, false, 0, 1>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
+            hipLaunchKernelGGL((k_band2bd_bundle<T, false>), dim3(grid), block, lds, s, A, n, lda, b, sg, S, R, magic, prog, err);
         return hipGetLastError();
     }
     const void *pfn = exact_order ? (const void *)k_band2bd_pipe<T, true> : (const void *)k_band2bd_pipe<T, false>;

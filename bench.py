@@ -348,9 +348,10 @@ def stage2_roofline(sw, n, b, dtype, steps):
 
 def plan_lanes(k: int, lmax: int = 10) -> int:
     """Stage-1 lanes for a stream of k matrices: the fewest rounds that
-    lmax lanes allow, dealt evenly (k = 20 -> 10 lanes x 2 rounds; 12 -> 6 x
-    2; 5 -> 5 x 1)."""
-    rounds = max(1, -(-k // lmax))
+    lmax lanes allow, but at least two (the first round's sweeps then run
+    beside the second round's stage 1 instead of all at the end), dealt
+    evenly (k = 20 -> 10 lanes x 2 rounds; 12 -> 6 x 2; 10 -> 5 x 2)."""
+    rounds = max(2 if k >= 4 else 1, -(-k // lmax))
     return max(1, -(-k // rounds))
 
 

@@ -222,6 +222,8 @@ def pmc_traffic(n: int, dtype: str, *kernel_prefixes: str):
     summary of this configuration is committed."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_n{n}_{dtype}.txt")))
+    # the newest summary that has this kernel at all
+    files = [f for f in files if any(ln.startswith(kernel_prefixes) for ln in open(f))]
     if not files:
         return None, None
     tot, cnt = 0.0, 0
@@ -285,7 +287,9 @@ def blkupd_roofline(bu, dtype, n):
     tf = bu["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     gbs = bu["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tn = "double" if dtype == "f64" else "float"
-    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_blkupd<" + tn, "void brd::blk::k_blkupd_p<" + tn)
+    # the persistent kernel only (the default since round 4): an older summary
+    # of the two-per-CU k_blkupd is another kernel's traffic
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_blkupd_p<" + tn)
     return {"kernel": "k_blkupd / k_blkupd_p (stage-1 delayed rank-256 trailing update, MFMA)", "bound": "mfma",
             "achieved": round(tf, 3), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
             "frac": round(tf / PEAK_TFLOPS[dtype], 4),
@@ -305,7 +309,7 @@ def rpass_roofline(rp, dtype, n):
     gbs = rp["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tf = rp["flops"] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     tn = "double" if dtype == "f64" else "float"
-    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_rpass<" + tn, "void brd::blk::k_rpass_d<" + tn)
+    traffic, src = pmc_traffic(n, dtype, "void brd::blk::k_rpass_d<" + tn)   # (the LDS-DMA pass, round 4 on)
     return {"kernel": "k_rpass / k_rpass_d (stage-1 read passes, MFMA)", "bound": "hbm", "achieved": round(gbs, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
             "traffic": round(traffic) if traffic else None, "traffic_source": src,

@@ -164,7 +164,9 @@ __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, in
     if (tl == 0) a.gew[grp] = (double)eg;
 }
 
-template <typename T>
+// JS >= 0 fixes the panel index j at compile time (the K1 chain then unrolls
+// without a uniform branch per step; JS = -1 reads it from the arguments)
+template <typename T, int JS>
 __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
     __shared__ __attribute__((aligned(16))) T Gt[32 * kLG];   // G^T over K1 (compact)
@@ -174,7 +176,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wi = a.split ? w & 1 : w, kh = a.split ? w >> 1 : 0;
     const int q = lane >> 4, l15 = lane & 15;
-    const int j = a.j, c = a.c;
+    const int j = JS >= 0 ? JS : a.j, c = a.c;
     const int nk1 = 64 * j, nk2 = 64 * j + 32;
     const T *G = (const T *)a.G;
     const T *Lw = (const T *)a.Lw;
@@ -366,7 +368,8 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     }
 }
 
-template <typename T>
+// JS / FS >= 0 fix j / a.factor at compile time (as k_prep_lq)
+template <typename T, int JS, int FS>
 __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
     typedef typename G2<T>::v2 v2;
@@ -377,9 +380,10 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
     const int w = a.split ? wk & 1 : wk, kh = a.split ? wk >> 1 : 0;   // item wave, K half
     const int q = lane >> 4, l15 = lane & 15;
-    const int j = a.j, jp = j - 1, c = a.c;
+    const int j = JS >= 0 ? JS : a.j, jp = j - 1, c = a.c;
+    const bool factor = FS >= 0 ? FS != 0 : a.factor != 0;
     const int n1 = 32 * j + 32 * jp;           // K1 compact: [0, 32j) | [128, 128 + 32jp)
-    const int n2 = a.factor ? 64 * j : 0;      // K2 compact: [0, 32j) | [128, 128 + 32j)
+    const int n2 = factor ? 64 * j : 0;      // K2 compact: [0, 32j) | [128, 128 + 32j)
     T *Rs = Gs + n1 * kQP;
     const T *G = (const T *)a.G;
     const T *RwT = (const T *)a.RwT;
@@ -396,7 +400,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ic = i0 + Mf<T>::crow(q, g);
-            ap[h][g] = (a.factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + a.cc + 16 * h + l15] : (T)0;
+            ap[h][g] = (factor && kh == 0 && ic < a.items) ? A[(size_t)(c + ic) * a.lda + a.cc + 16 * h + l15] : (T)0;
         }
     // ranges of Lw columns: [0, 32j) (compact 0; K half 0) and [128, 128 + 32jp)
     // (compact 32j; K half 1); lane q takes k = 8s + 2q + e.  All A operands
@@ -460,7 +464,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         ax[h] = Mf<T>::mma(x, Gs[kk * kQP + 16 * h + l15], ax[h]);
-                        if (a.factor) ap[h] = Mf<T>::mma(x, Rs[kk * kQP + 16 * h + l15], ap[h]);
+                        if (factor) ap[h] = Mf<T>::mma(x, Rs[kk * kQP + 16 * h + l15], ap[h]);
                     }
                 }
             }
@@ -521,7 +525,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
             const int r = Mf<T>::crow(q, g), t = 16 * h + l15;
             // the pass used U' = Q: ap here is A_cur[row][c + t] (corrections;
             // the block end's reduce-only call follows an inline finish: none)
-            const T corr = a.factor ? (T)a.sgn[t] * ap[h][g] : (T)0;
+            const T corr = factor ? (T)a.sgn[t] * ap[h][g] : (T)0;
             Tb[w][r * 34 + t] = (i0 + r < a.items) ? xs[h][g] - ax[h][g] - corr : (T)0;
         }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -546,7 +550,7 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
             if (ic < a.items) Lw[(size_t)(c + ic) * 256 + 128 + 32 * jp + t] = xx[h][g];
             Tb[w][r * 34 + t] = xx[h][g];
         }
-    if (!a.factor) return;
+    if (!factor) return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -594,8 +598,25 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 
 template <typename T>
 void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s) {
-    if (lq) blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T>, grid, dim3(kPT), s, p);
-    else    blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T>, grid, dim3(kPT), s, p);
+    static_assert(NBMAX == 4, "the specialised panel indices below");
+    if (lq) {
+        switch (p.j) {
+        case 0: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 0>, grid, dim3(kPT), s, p); return;
+        case 1: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 1>, grid, dim3(kPT), s, p); return;
+        case 2: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 2>, grid, dim3(kPT), s, p); return;
+        case 3: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 3>, grid, dim3(kPT), s, p); return;
+        default: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, -1>, grid, dim3(kPT), s, p); return;
+        }
+    }
+    // the one-GPU and distributed drivers call (j, factor) = (1..3, 1) per
+    // panel and (4, 0) at the block end
+    switch (p.factor ? p.j : -p.j) {
+    case 1: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 1, 1>, grid, dim3(kPT), s, p); return;
+    case 2: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 2, 1>, grid, dim3(kPT), s, p); return;
+    case 3: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 3, 1>, grid, dim3(kPT), s, p); return;
+    case -4: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 4, 0>, grid, dim3(kPT), s, p); return;
+    default: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, -1, -1>, grid, dim3(kPT), s, p); return;
+    }
 }
 template void launch_k_prep<double>(bool, dim3, const PrepArgs &, hipStream_t);
 template void launch_k_prep<float>(bool, dim3, const PrepArgs &, hipStream_t);

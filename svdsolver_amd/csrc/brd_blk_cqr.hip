@@ -387,6 +387,24 @@ __global__ void __launch_bounds__(kCT, 1) k_cqr_gram(CqrArgs a) {
     if (coh) cqr_to_record(L, a, W.gp1, W.ew, 0);
 }
 
+// BRD_CQR_STAMPS (diagnostic builds, tools/cqr_stamps.py): per-workgroup
+// phase timestamps of the k_cqr_v launches whose a.M equals the target the
+// host set (k_cqr_v's register allocation is unchanged by them; stamps in
+// k_cqr_q1 made it spill, so it has none)
+#ifdef BRD_CQR_STAMPS
+__device__ unsigned long long g_cqr_st[64][12];
+__device__ long g_cqr_target;
+#define CQR_ST(P)                                                                          \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 64 && (long)a.M == g_cqr_target)               \
+            g_cqr_st[blockIdx.x][P] = __builtin_amdgcn_s_memrealtime();                    \
+    } while (0)
+#else
+#define CQR_ST(P) \
+    do {          \
+    } while (0)
+#endif
+
 template <typename T>
 __global__ void __launch_bounds__(kCT, 1) k_cqr_q1(CqrArgs a) {
     __shared__ CqrLdsS L;
@@ -659,9 +677,11 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
     __shared__ CqrLds L;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wg = blockIdx.x, nwg = gridDim.x;
     CqrWs W(a.ws);
+    CQR_ST(0);
     if (tid == 0) L.flags = 0;
     const GramSrc g1 = cqr_gram_src(a, 0, W.gp1, W.ew);
     const int e = cqr_exponent(L, g1.ew, g1.n, true, g1.es);   // (L.scl: ones)
+    CQR_ST(1);
     const bool zero = e == INT_MIN;   // V = [I; 0], T = 0, R = 0
     const int i = wg * kCT + tid;
     T *ap = (T *)a.apan;
@@ -681,6 +701,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
             gram_sum_all(L, g2.gp, L.scl, g2.n, g2.gs);
         }
         __syncthreads();
+        CQR_ST(2);
         // G2 = Q1^T Q1 = I + E with E ~ cond(P)^2 eps.  When max|E| < 1e-8 the
         // Cholesky factor is I + U1 + O(E^2) (U1: the upper triangle of E with
         // half its diagonal) and its inverse I - U1 + O(E^2): both to working
@@ -708,9 +729,11 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
             if (lane == 0 && !good) L.flags = 1;
         }
         __syncthreads();
+        CQR_ST(3);
         // Q = Q1 R2^-1, this thread's row
         if (fast) umul_row(x, L.r2w);
         else      trsm_row(x, L.r2w);
+        CQR_ST(4);
         if (i >= a.M) {
 #pragma unroll
             for (int t = 0; t < 32; ++t) x[t] = 0.0;
@@ -764,6 +787,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         }
     };
     store_v(x, 0, INT_MAX);   // V' = Q (the top rows get - S after the LU: k_vsum)
+    CQR_ST(5);
     if (a.azero) {   // zeros below the panel's R block
         typedef typename G2<T>::v2 v2;
         const int zlo = a.top ? 32 : 0;
@@ -780,6 +804,7 @@ __global__ void __launch_bounds__(kCT, 1) __attribute__((amdgpu_waves_per_eu(1, 
         }
     }
     if (L.flags && tid == 0) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CQR_ST(6);
     if (wg != 0) return;
 
     // ---- workgroup 0: Q_t and the zero flag for the LU (k_rpass's finishing
@@ -847,3 +872,15 @@ template void launch_k_cqr<float>(CqrKernel, int, const CqrArgs &, const FinArgs
 
 }  // namespace blk
 }  // namespace brd
+
+#ifdef BRD_CQR_STAMPS
+extern "C" int brd_debug_cqr_target(long m) {   // and clears the stamps
+    static unsigned long long zero[64 * 12];
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(brd::blk::g_cqr_st), zero, sizeof(zero));
+    if (e != hipSuccess) return (int)e;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(brd::blk::g_cqr_target), &m, sizeof(m));
+}
+extern "C" int brd_debug_cqr_stamps(unsigned long long *out) {   // [64][12] ticks of 10 ns
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(brd::blk::g_cqr_st), sizeof(brd::blk::g_cqr_st));
+}
+#endif

@@ -228,7 +228,18 @@ __global__ void __launch_bounds__(256) k_vsum(const T *vpart, T *vout, int nvirt
 #ifndef BRD_RPASS_HOIST
 #define BRD_RPASS_HOIST 0   // A/B knob (tools/variant_lib.sh): 1 measured no faster (X pass 110 -> 113 us)
 #endif
-constexpr int kRS = 4;      // stages in flight
+// stages in the ring (kRS - 1 in flight).  Round 6, N = 8192 fp64 one at a
+// time, same box: rings of 2 / 3 / 4 stages 21.45 / 21.25 / 21.72-21.84 ms of
+// read passes per matrix, the stream unchanged; the next stage's DMAs spread
+// between the MFMA steps 22.7, the source stream non-temporal 21.8 -- the
+// large passes are not bound by the bytes in flight or the DMA issue
+constexpr int kRS = 4;
+// wait until at most `younger` stages' DMAs are outstanding (waves 0-3 issue
+// 5 a stage, 4-7 issue 4; vmcnt counts in order)
+template <int Y> __device__ __forceinline__ void rp_wait(bool five) {
+    if (five) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * Y) : "memory");
+    else      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * Y) : "memory");
+}
 constexpr int kSY = 272;    // Y stage pitch (elements per k row: rows k..k+3 of a read in distinct banks)
 struct RpLdsD {             // 32 KB of source + 4 KB of B per stage, either type
     double s[kRS][16 * kSY];    // Y [k][272]; X [256][kRK]
@@ -292,32 +303,32 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
         //   X: instruction i covers rows 8i..8i+7, 128 B each (lane: row
         //      8i + lane / 8, 16-B slot lane & 7)
         //   B: wave w's instruction covers rows BRI w .. BRI w + BRI - 1
-        auto issue = [&](int st) {
+        auto issue_src = [&](int st, int uu) {   // source piece uu (of 4) of stage st
             const int k0 = kb0 + KRK * st, buf = st % kRS;
             if constexpr (YP) {
                 const u32x4_t rs = rsrc_of(S + (long)k0 * ld);
                 constexpr int IPR = 256 * E / 1024;    // instructions per row
-#pragma unroll
-                for (int uu = 0; uu < 4; ++uu) {
-                    const int i = 4 * w + uu, kr = i / IPR, h = i % IPR, m = (1024 * h + 16 * lane) / E;
-                    const unsigned off = (k0 + kr < ke0 && m < M) ? (unsigned)((kr * (int)ld + m) * E) : kOut;
-                    dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + (kr * kSY + 1024 / E * h) * E));
-                }
+                const int i = 4 * w + uu, kr = i / IPR, h = i % IPR, m = (1024 * h + 16 * lane) / E;
+                const unsigned off = (k0 + kr < ke0 && m < M) ? (unsigned)((kr * (int)ld + m) * E) : kOut;
+                dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + (kr * kSY + 1024 / E * h) * E));
             } else {
                 const u32x4_t rs = rsrc_of(S + k0);
+                const int i = 4 * w + uu, m = 8 * i + (lane >> 3), sl = lane & 7, pr = sl ^ ((m >> 1) & 7);
+                const unsigned off = (m < M && k0 + EPV * pr < ke0) ? (unsigned)((m * (int)ld + EPV * pr) * E) : kOut;
+                dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + i * 1024));
+            }
+        };
+        auto issue_b = [&](int st) {   // waves 0-3: their B piece of stage st
+            const int k0 = kb0 + KRK * st, buf = st % kRS;
+            const u32x4_t rb = rsrc_of(B + (long)k0 * a.bld);
+            const int kr = BRI * w + lane / BVR, sl = lane % BVR, tp = sl ^ rp_bswz<T>(kr);
+            const unsigned off = k0 + kr < ke0 ? (unsigned)((kr * (int)a.bld + EPV * tp) * E) : kOut;
+            dma16(rb, off, 0, lds_b + (unsigned)(buf * sizeof(L.b[0]) + w * 1024));
+        };
+        auto issue = [&](int st) {
 #pragma unroll
-                for (int uu = 0; uu < 4; ++uu) {
-                    const int i = 4 * w + uu, m = 8 * i + (lane >> 3), sl = lane & 7, pr = sl ^ ((m >> 1) & 7);
-                    const unsigned off = (m < M && k0 + EPV * pr < ke0) ? (unsigned)((m * (int)ld + EPV * pr) * E) : kOut;
-                    dma16(rs, off, 0, lds_s + (unsigned)(buf * sizeof(L.s[0]) + i * 1024));
-                }
-            }
-            if (w < 4) {
-                const u32x4_t rb = rsrc_of(B + (long)k0 * a.bld);
-                const int kr = BRI * w + lane / BVR, sl = lane % BVR, tp = sl ^ rp_bswz<T>(kr);
-                const unsigned off = k0 + kr < ke0 ? (unsigned)((kr * (int)a.bld + EPV * tp) * E) : kOut;
-                dma16(rb, off, 0, lds_b + (unsigned)(buf * sizeof(L.b[0]) + w * 1024));
-            }
+            for (int uu = 0; uu < 4; ++uu) issue_src(st, uu);
+            if (w < 4) issue_b(st);
         };
 
         v4 acc[2][2];
@@ -332,17 +343,14 @@ __global__ void __launch_bounds__(kRT, 1) k_rpass_d(RpArgs a, FinArgs fin) {
             // this stage's DMAs landed: the younger stages' (up to kRS - 2) may still fly
             // (in-order vmcnt; waves 0-3 issue 5 DMAs a stage, waves 4-7 issue 4)
             const int younger = min(nst - 1 - st, kRS - 2);
-            if (younger >= 2) {
-                if (w < 4) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-                else       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            } else if (younger == 1) {
-                if (w < 4) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-                else       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            static_assert(kRS >= 2 && kRS <= 5, "rp_wait cases");
+            if (kRS >= 5 && younger >= 3) rp_wait<3>(w < 4);
+            else if (kRS >= 4 && younger >= 2) rp_wait<2>(w < 4);
+            else if (kRS >= 3 && younger >= 1) rp_wait<1>(w < 4);
+            else rp_wait<0>(w < 4);
             __syncthreads();
-            if (st + kRS - 1 < nst) issue(st + kRS - 1);   // into the buffer every wave finished reading
+            // into the buffer every wave finished reading
+            if (st + kRS - 1 < nst) issue(st + kRS - 1);
             const int buf = st % kRS;
             const T *ls = (const T *)L.s[buf], *lb = (const T *)L.b[buf];
             // every operand of the stage first (one LDS latency per stage, not

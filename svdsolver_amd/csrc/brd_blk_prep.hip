@@ -164,15 +164,33 @@ __device__ __forceinline__ void prep_gram(const PrepArgs &a, int nwv, int wv, in
     if (tl == 0) a.gew[grp] = (double)eg;
 }
 
-// JS >= 0 fixes the panel index j at compile time (the K1 chain then unrolls
-// without a uniform branch per step; JS = -1 reads it from the arguments)
+// JS >= 0 fixes the panel index j at compile time: the K1 chain then unrolls
+// without a uniform branch per step, and the LDS holds only what panel j
+// needs (pitches 64 j + 2 / 64 j + 34, the same residues mod 64 as kLG / kLW,
+// so the same bank pattern), so the early panels' kernels co-reside two or
+// three to a CU in a stream; JS = -1 reads j from the arguments.
+// (the K1 staging block also holds the split halves' hand-off Xh and then
+// prep_gram's wave tiles, both after the K1 chain.  T_j^T moved there as
+// well -- panel 2's kernel in 75 KB instead of 83 -- measured no faster in the
+// stream: 26.87 / 27.06 against 26.99 / 27.04 TFLOP/s, same box)
+constexpr int kGramTileB = 4 * 16 * 33 * 8, kGramRedB = 32 * 33 * 8;   // prep_gram's two LDS blocks
+template <typename T, int JS> struct LqLds {
+    static constexpr int LG = JS >= 0 ? 64 * JS + 2 : kLG, LW = JS >= 0 ? 64 * JS + 34 : kLW;
+    static constexpr int cmax(int x, int y) { return x > y ? x : y; }
+    static constexpr int GB = cmax(cmax(32 * LG * (int)sizeof(T), kGramTileB), 2 * 16 * 64 * (int)sizeof(T));
+    static constexpr int WB = cmax(32 * LW * (int)sizeof(T), kGramRedB);
+};
 template <typename T, int JS>
 __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
-    __shared__ __attribute__((aligned(16))) T Gt[32 * kLG];   // G^T over K1 (compact)
-    __shared__ __attribute__((aligned(16))) T Lt[32 * kLW];   // -Lw[c+t][k] over K2 (compact)
+    typedef LqLds<T, JS> LD;
+    constexpr int LG = LD::LG, LW = LD::LW;
+    __shared__ __attribute__((aligned(16))) unsigned char gt_raw[LD::GB];
+    __shared__ __attribute__((aligned(16))) unsigned char lt_raw[LD::WB];
+    T *Gt = reinterpret_cast<T *>(gt_raw);   // G^T over K1 (compact), pitch LG
+    T *Lt = reinterpret_cast<T *>(lt_raw);   // -Lw[c+t][k] over K2 (compact), pitch LW
     __shared__ T Tt[32 * 34];    // T_j^T
-    __shared__ T Xh[2][16][64];  // the second K half's accumulators
+    T (*Xh)[16][64] = reinterpret_cast<T (*)[16][64]>(gt_raw);   // the second K half's accumulators
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wi = a.split ? w & 1 : w, kh = a.split ? w >> 1 : 0;
     const int q = lane >> 4, l15 = lane & 15;
@@ -222,7 +240,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
 #pragma unroll
         for (int t = 0; t < 32; ++t) v[t] = G[(size_t)t * 256 + k];
 #pragma unroll
-        for (int t = 0; t < 32; ++t) Gt[t * kLG + kk] = v[t];
+        for (int t = 0; t < 32; ++t) Gt[t * LG + kk] = v[t];
     }
     if (tid < nk2) {
         const int kk = tid, k = kk < 32 * (j + 1) ? kk : 128 + kk - 32 * (j + 1);
@@ -235,7 +253,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
                 if (k == 32 * j + t) v[t] = (T)((double)v[t] - a.sgn[t]);
         }
 #pragma unroll
-        for (int t = 0; t < 32; ++t) Lt[t * kLW + kk] = -v[t];
+        for (int t = 0; t < 32; ++t) Lt[t * LW + kk] = -v[t];
     }
     {
         T v[4];
@@ -258,13 +276,14 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
                 const int kk = 4 * s + q;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * kLG + gb + kk], bk[pp][s], ay[h]);
-                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + lb + kk], bk[pp][s], aq[h]);
+                    ay[h] = Mf<T>::mma(Gt[(16 * h + l15) * LG + gb + kk], bk[pp][s], ay[h]);
+                    aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * LW + lb + kk], bk[pp][s], aq[h]);
                 }
             }
         }
     }
     if (a.split) {   // the halves meet: kh = 1 hands its sums over and is done
+        __syncthreads();   // (Xh overlays G^T: both halves' K1 chains are done)
         if (kh) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -344,7 +363,7 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
         for (int g = 0; g < 4; ++g) {
             const int u = 16 * hp + Mf<T>::crow(q, g);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * kLW + 32 * j + u], ayj[hp][g], aq[h]);
+            for (int h = 0; h < 2; ++h) aq[h] = Mf<T>::mma(Lt[(16 * h + l15) * LW + 32 * j + u], ayj[hp][g], aq[h]);
         }
     T *QpT = (T *)a.Qp;
 #pragma unroll
@@ -368,12 +387,20 @@ __global__ void __launch_bounds__(kPT) k_prep_lq(PrepArgs a) {
     }
 }
 
-// JS / FS >= 0 fix j / a.factor at compile time (as k_prep_lq)
+// JS / FS >= 0 fix j / a.factor at compile time (as k_prep_lq): the staging
+// block holds the K1 + K2 rows of that panel only (32 j + 32 (j - 1) +
+// 64 j factor; 352 at most), and at least prep_gram's two blocks
+template <typename T, int JS, int FS> struct QrLds {
+    static constexpr int ROWS = JS >= 0 && FS >= 0 ? 32 * JS + 32 * (JS - 1) + (FS ? 64 * JS : 0) : 352;
+    static constexpr int B = ROWS * kQP * (int)sizeof(T) > kGramTileB + kGramRedB ? ROWS * kQP * (int)sizeof(T)
+                                                                                  : kGramTileB + kGramRedB;
+};
 template <typename T, int JS, int FS>
 __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
     typedef typename Mf<T>::v4 v4;
     typedef typename G2<T>::v2 v2;
-    __shared__ __attribute__((aligned(16))) T Gs[352 * kQP];      // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
+    __shared__ __attribute__((aligned(16))) unsigned char gs_raw[QrLds<T, JS, FS>::B];
+    T *Gs = reinterpret_cast<T *>(gs_raw);   // G over K1 (compact), then -RwT[k][c+t] over K2 (compact)
     __shared__ T Ss[32 * 48];        // S_{j-1}
     __shared__ T Tb[4][16 * 34];     // per-wave transpose of x / X_{j-1}
     __shared__ T Xh[2][16][64];      // the second K half's accumulators

@@ -1,12 +1,16 @@
 """Bitwise A/B of two builds of the library (developer tool): stage 1 and the
 compat stage 2 of the same seeded N x N matrix through each library's C ABI.
-usage: python tools/ab_bitwise.py <libA.so> <libB.so> [n=2048] [f64|f32]"""
+usage: [BRD_AB_OVERLAP=CUS] python tools/ab_bitwise.py <libA.so> <libB.so> [n=2048] [f64|f32]"""
 import ctypes
+import os
 import sys
 
 import torch
 
 libs = [ctypes.CDLL(p) for p in sys.argv[1:3]]
+ov = int(os.environ.get("BRD_AB_OVERLAP", "0"))   # > 0: stage 1 sized beside a stage-2 reservation (stream form)
+for L in libs:
+    assert L.brd_set_overlap(ov) == 0
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
 dt = torch.float32 if (len(sys.argv) > 4 and sys.argv[4] == "f32") else torch.float64
 sfx = "f32" if dt == torch.float32 else "f64"

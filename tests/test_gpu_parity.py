@@ -365,6 +365,7 @@ def test_reduce_many_pipelined_matches_serial(S, lanes):
     # stage 1 alone under the overlap setting (the remaining-CU launch sizes)
     mats = [torch.from_numpy(A).cuda() for A in As]
     s_a = torch.cuda.Stream()
+    s_a.wait_stream(torch.cuda.current_stream())   # the copies ran on the default stream
     S.set_overlap(S.overlap_cus(n))
     try:
         with torch.cuda.stream(s_a):
@@ -415,6 +416,7 @@ def test_stage1_f32_overlap_matches_serial(S):
         ref.append(dA.cpu().numpy())
     mats = [torch.from_numpy(A).cuda() for A in As]
     s_a = torch.cuda.Stream()
+    s_a.wait_stream(torch.cuda.current_stream())   # the copies ran on the default stream
     S.set_overlap(S.overlap_cus(n))
     try:
         with torch.cuda.stream(s_a):
@@ -604,6 +606,7 @@ def test_release_stream_frees_and_keeps_working(S):
     import torch
     A = torch.rand(512, 512, dtype=torch.float64, device="cuda") * 5
     st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())   # A was written on the default stream
     with torch.cuda.stream(st):
         M = A.clone()
         S.ge2band(M, 32, sync=False)

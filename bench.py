@@ -632,6 +632,8 @@ def main():
     torch.cuda.synchronize(dev)
     S.check_errors()
 
+    host_issue_ms = []
+
     def run_steps(first):
         """K steps bracketed by barrier + synchronize; per-step stage split by
         events on the launch stream.  Returns (elapsed, stage1 ms, stage2 ms)."""
@@ -642,6 +644,7 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         issue(first, args.steps, ev)
+        host_issue_ms.append(1e3 * (time.perf_counter() - t0))   # the host's launch calls (diagnostic)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -748,6 +751,8 @@ def main():
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "rccl_nranks": world if (dist_mode and args.comm == "rccl") else None},
             "latency_ms_per_reduction": round(s1 + s2, 3),
+            # host time to issue the K steps' launches: the timed pass (, one at a time, profiled)
+            "host_issue_ms": [round(x, 1) for x in host_issue_ms],
             "one_at_a_time": one_at_a_time,
             "stage_ms": {"stage1": round(s1, 3), "stage2": round(s2, 3)},
             "profiled_ms_per_step": round(el_prof / args.steps * 1e3, 3),

@@ -2,6 +2,7 @@
 #include "brd_blk.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace brd {
 namespace blk {
@@ -626,8 +627,12 @@ __global__ void __launch_bounds__(kPT) k_prep_qr(PrepArgs a) {
 template <typename T>
 void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s) {
     static_assert(NBMAX == 4, "the specialised panel indices below");
+    // BRD_PREP_GENERIC=1: the run-time-j forms only (read per launch: the
+    // parity test compares the two bit for bit)
+    const char *ge = getenv("BRD_PREP_GENERIC");
+    const int jsel = (ge && atoi(ge) != 0) ? -100 : p.j;
     if (lq) {
-        switch (p.j) {
+        switch (jsel) {
         case 0: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 0>, grid, dim3(kPT), s, p); return;
         case 1: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 1>, grid, dim3(kPT), s, p); return;
         case 2: blk_launch("s1_prep", 0.0, 0.0, k_prep_lq<T, 2>, grid, dim3(kPT), s, p); return;
@@ -637,7 +642,7 @@ void launch_k_prep(bool lq, dim3 grid, const PrepArgs &p, hipStream_t s) {
     }
     // the one-GPU and distributed drivers call (j, factor) = (1..3, 1) per
     // panel and (4, 0) at the block end
-    switch (p.factor ? p.j : -p.j) {
+    switch (jsel == -100 ? -100 : (p.factor ? p.j : -p.j)) {
     case 1: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 1, 1>, grid, dim3(kPT), s, p); return;
     case 2: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 2, 1>, grid, dim3(kPT), s, p); return;
     case 3: blk_launch("s1_prep", 0.0, 0.0, k_prep_qr<T, 3, 1>, grid, dim3(kPT), s, p); return;

@@ -598,6 +598,34 @@ def test_blkupd_xcd_order_bitwise(S, m, n, T):
     assert np.array_equal(B0, B1)
 
 
+@pytest.mark.parametrize("n,T,overlap", [(1000, "double", False), (2080, "double", True), (1536, "float", False),
+                                         (2048, "float", True)])
+def test_prep_specialised_bitwise(S, n, T, overlap):
+    """The prep kernels specialised per panel index (k_prep_lq<T, j>,
+    k_prep_qr<T, j, factor>: compile-time K chains, LDS sized for panel j)
+    give the band of the run-time-j forms (BRD_PREP_GENERIC=1) BIT FOR BIT,
+    one at a time (split K halves) and beside a stage-2 reservation (the
+    stream's unsplit form, the early panels' smaller LDS)."""
+    import os
+    rng = np.random.default_rng(11 * n)
+    A = (rng.random((n, n)) * 4 + 1).astype(np.float64 if T == "double" else np.float32)
+    old = os.environ.get("BRD_PREP_GENERIC")
+    if overlap:
+        S.set_overlap(S.overlap_cus(n))
+    try:
+        os.environ["BRD_PREP_GENERIC"] = "1"
+        B0 = S.brd_p1(A, 32)
+        os.environ["BRD_PREP_GENERIC"] = "0"
+        B1 = S.brd_p1(A, 32)
+    finally:
+        S.set_overlap(0)
+        if old is None:
+            os.environ.pop("BRD_PREP_GENERIC", None)
+        else:
+            os.environ["BRD_PREP_GENERIC"] = old
+    assert np.array_equal(B0, B1)
+
+
 def test_release_stream_frees_and_keeps_working(S):
     """brd_release_stream: a stream the library launched on can be released
     (drained, its workspaces and error word freed) and destroyed; a later

@@ -12,6 +12,6 @@ if [ "$dt" = "f64" ]; then mops=SQ_INSTS_VALU_MFMA_MOPS_F64; else mops=SQ_INSTS_
 i=0
 for c in FETCH_SIZE WRITE_SIZE "$mops SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${tag}_n${n}_${dt}_p$i -o run -- python3 bench.py --n $n --dtype $dt --steps 1 --warmup 1 --cpu-baseline off --pipeline off ${extra//,/ } > gpurun_out/pmc_${tag}_n${n}_${dt}_p$i.log 2>&1 || { echo "PMC pass $i ($c) FAILED"; tail -5 gpurun_out/pmc_${tag}_n${n}_${dt}_p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${tag}_n${n}_${dt}_p$i -o run -- python3 bench.py --n $n --dtype $dt --steps 1 --warmup ${PMC_WARMUP:-1} --cpu-baseline off --pipeline off ${extra//,/ } > gpurun_out/pmc_${tag}_n${n}_${dt}_p$i.log 2>&1 || { echo "PMC pass $i ($c) FAILED"; tail -5 gpurun_out/pmc_${tag}_n${n}_${dt}_p$i.log; exit 1; }
 done
 python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_n${n}_${dt}_p1 gpurun_out/pmc_${tag}_n${n}_${dt}_p2 gpurun_out/pmc_${tag}_n${n}_${dt}_p3 $dt | tee gpurun_out/pmc_${tag}_n${n}_${dt}.txt

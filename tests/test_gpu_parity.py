@@ -691,13 +691,14 @@ def test_stage2_shrinking_grid_bitwise(S, n, dt, monkeypatch):
     8, 4 workgroups as the chain's live bundles fall) changes only which
     workgroup runs a bundle, never the arithmetic or the hand-off order: the
     bidiagonal is the one-stage grid's bit for bit, beside a stage-2
-    reservation (32 workgroups, the stream's grid) and without one."""
+    reservation (32 workgroups, the stream's grid), without one, and with
+    grids whose halvings end early or oddly (24: 12, 6; 40: 20, 10, 5)."""
     import torch
     b = 32
     tdt = torch.float64 if dt == "f64" else torch.float32
     A = torch.from_numpy(np.random.default_rng(n).uniform(0, 5, (n, n))).to(tdt).cuda()
     S.ge2band(A, b)
-    for cus in (0, S.overlap_cus(n)):
+    for cus in (0, S.overlap_cus(n), 24, 40):
         out = []
         S.set_overlap(cus)
         try:
